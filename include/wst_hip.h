@@ -1,0 +1,105 @@
+/*
+ * wst_hip.h -- C ABI of the MI355X-native 2-D wavelet scattering transform (WST).
+ *
+ * Drop-in boundary for the reference's WST feature path.  The reference reaches kymatio 0.3.0's
+ * Scattering2D from these call sites (all file:line into the reference repository):
+ *   - src/training/train_and_save_model.py:46   `from kymatio.numpy import Scattering2D`
+ *   - src/training/train_and_save_model.py:359  `Scattering2D(J=J, L=L, shape=(H, W))`
+ *   - src/training/train_and_save_model.py:368  `scattering(channel)`            (H,W)->(K,H',W')
+ *   - src/training/train_and_save_model.py:371-375 per-coefficient spatial mean/std pooling
+ *   - src/inference/inference.py:39,242,254     torch frontend `S(channel_tensor)` (1,1,H,W)
+ *   - src/visualization/compare_wst_coefficients.py:37 `Scattering2D(..., frontend='numpy')`
+ * kymatio is pure Python, so the "FFI" this library replaces is the Python-level operator API;
+ * the Python frontends in wst_amd/ bind these symbols with ctypes.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  Device pointers are HIP device allocations (e.g. torch
+ *     tensors' data_ptr()).  `stream` is a hipStream_t passed as void* (0 = null stream).
+ *   - Every entry point returns an int status (WST_OK = 0).  No C++ exception crosses the ABI.
+ *     wst_last_error() returns a thread-local, NUL-terminated description of the last failure.
+ *   - A plan is immutable after creation and bound to the device that was current at creation.
+ *     wst_forward is asynchronous on `stream` and re-entrant across streams when each call gets
+ *     its own workspace.
+ */
+#ifndef WST_HIP_H
+#define WST_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WST_ABI_VERSION 1
+
+enum wst_status {
+    WST_OK = 0,
+    WST_ERR_INVALID = 1,     /* bad argument (maps to RuntimeError/TypeError in the frontends) */
+    WST_ERR_UNSUPPORTED = 2, /* size/config the kernels do not implement                        */
+    WST_ERR_HIP = 3,         /* HIP runtime error (launch, copy, device mismatch)               */
+    WST_ERR_NOMEM = 4        /* host or device allocation failed                                */
+};
+
+typedef struct wst_plan wst_plan;
+
+/* ABI version of the loaded library (== WST_ABI_VERSION of the header it was built with). */
+int wst_abi_version(void);
+
+/* Thread-local description of the last error ("" if none). */
+const char* wst_last_error(void);
+
+/*
+ * Build a plan for Scattering2D(J, shape=(M, N), L, max_order, pre_pad).
+ * Replaces kymatio 0.3.0 ScatteringBase2D.build()/create_filters() (reached from
+ * train_and_save_model.py:359 and inference.py:242): padding (compute_padding), the Morlet/Gabor
+ * filter bank built on the host in float64 (filter_bank, masked-crop levels), uploaded once as
+ * fp32, plus twiddle tables.  Errors: 2^J > min(M, N) -> WST_ERR_INVALID (kymatio raises
+ * RuntimeError); max_order not in {1, 2} -> WST_ERR_INVALID.
+ */
+int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_plan** out);
+
+/* Release the plan and its device memory. NULL is accepted. */
+int wst_plan_destroy(wst_plan* plan);
+
+/* Output geometry: K coefficients of (Mo, No) = (M / 2^J, N / 2^J); padded grid (PM, PN). */
+int wst_output_shape(const wst_plan* plan, int* K, int* Mo, int* No);
+int wst_padded_shape(const wst_plan* plan, int* PM, int* PN);
+
+/* Bytes of device workspace wst_forward needs to process `nbatch` planes in one pass.
+ * Any smaller (non-zero) workspace is accepted: the batch is then processed in chunks. */
+int wst_workspace_bytes(const wst_plan* plan, int64_t nbatch, size_t* bytes);
+
+/*
+ * Scattering of `nbatch` float32 planes.
+ *   d_in  : device, nbatch x M x N (or PM x PN if pre_pad), contiguous.
+ *   d_out : device, pooled == 0 -> nbatch x K x Mo x No   (kymatio `S(x)` layout, stack order
+ *                                   [S0; S1 (j1,l1); S2 (j1,l1,j2>j1,l2)])
+ *                   pooled == 1 -> nbatch x 2K: per plane [mean_k (K) | std_k (K)], population
+ *                                   std over (Mo, No) -- train_and_save_model.py:371-375 order.
+ *   d_workspace / workspace_bytes : caller-owned scratch (see wst_workspace_bytes); NULL/0 lets
+ *                   the plan use an internal buffer (allocated on first use; not graph-capturable).
+ *   stream : hipStream_t as void*.
+ * Replaces: kymatio scattering2d() over the flattened batch (one call on (B,C,H,W) replaces the
+ * reference's B*C serial calls at train_and_save_model.py:364-368 / inference.py:248-254).
+ */
+int wst_forward(const wst_plan* plan, const float* d_in, int64_t nbatch, float* d_out, int pooled,
+                void* d_workspace, size_t workspace_bytes, void* stream);
+
+/*
+ * Host-only filter inspection (no GPU needed; used by the CPU test-suite to pin the library's
+ * float64 filter construction against the oracle).  kind:
+ *   0 = psi_{j,l} Fourier level r        -> (PM>>r) x (PN>>r) doubles
+ *   1 = phi Fourier level r (2-D)        -> (PM>>r) x (PN>>r) doubles (separable product)
+ *   2 = phi spatial low-pass, rows (M)   -> (PM>>r) doubles
+ *   3 = phi spatial low-pass, cols (N)   -> (PN>>r) doubles
+ * `len` is the capacity of `out` in doubles.
+ */
+int wst_host_filter(int M, int N, int J, int L, int kind, int j, int l, int r, double* out,
+                    int64_t len);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WST_HIP_H */

@@ -1,0 +1,139 @@
+"""ctypes binding of the in-tree C-ABI library ``libwst_hip.so`` (include/wst_hip.h).
+
+There is no CPU fallback: if the library is missing, or no ROCm GPU is visible, every compute
+entry point raises ``RuntimeError``.  Only the host-side filter inspection
+(``host_filter``) runs without a GPU (it is pure C++ float64 code inside the same library).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+LIB_NAME = "libwst_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+WST_OK, WST_ERR_INVALID, WST_ERR_UNSUPPORTED, WST_ERR_HIP, WST_ERR_NOMEM = 0, 1, 2, 3, 4
+ABI_VERSION = 1
+
+# every symbol include/wst_hip.h declares
+EXPORTS = (
+    "wst_abi_version", "wst_last_error", "wst_plan_create", "wst_plan_destroy",
+    "wst_output_shape", "wst_padded_shape", "wst_workspace_bytes", "wst_forward",
+    "wst_host_filter",
+)
+
+_lib = None
+_lock = threading.Lock()
+
+
+class WSTError(RuntimeError):
+    """Raised for a non-zero status from the C ABI."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and type the library.  Raises RuntimeError if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_NAME} not found at {LIB_PATH}: the HIP extension is not built "
+                "(run `python -c 'import __graft_entry__ as g; g.build()'` or `make -C <pkg>/csrc`)")
+        lib = ctypes.CDLL(LIB_PATH)
+        c_int, c_i64, c_vp, c_sz = ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t
+        lib.wst_abi_version.restype = c_int
+        lib.wst_abi_version.argtypes = []
+        lib.wst_last_error.restype = ctypes.c_char_p
+        lib.wst_last_error.argtypes = []
+        lib.wst_plan_create.restype = c_int
+        lib.wst_plan_create.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int,
+                                        ctypes.POINTER(c_vp)]
+        lib.wst_plan_destroy.restype = c_int
+        lib.wst_plan_destroy.argtypes = [c_vp]
+        lib.wst_output_shape.restype = c_int
+        lib.wst_output_shape.argtypes = [c_vp] + [ctypes.POINTER(c_int)] * 3
+        lib.wst_padded_shape.restype = c_int
+        lib.wst_padded_shape.argtypes = [c_vp] + [ctypes.POINTER(c_int)] * 2
+        lib.wst_workspace_bytes.restype = c_int
+        lib.wst_workspace_bytes.argtypes = [c_vp, c_i64, ctypes.POINTER(c_sz)]
+        lib.wst_forward.restype = c_int
+        lib.wst_forward.argtypes = [c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_sz, c_vp]
+        lib.wst_host_filter.restype = c_int
+        lib.wst_host_filter.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                        ctypes.POINTER(ctypes.c_double), c_i64]
+        v = lib.wst_abi_version()
+        if v != ABI_VERSION:
+            raise RuntimeError(f"{LIB_NAME} ABI version {v} != expected {ABI_VERSION}; rebuild it")
+        _lib = lib
+        return lib
+
+
+def last_error() -> str:
+    return load().wst_last_error().decode(errors="replace")
+
+
+def check(code: int) -> None:
+    if code != WST_OK:
+        raise WSTError(code, last_error() or f"wst status {code}")
+
+
+def host_filter(M, N, J, L, kind, j, l, r, size) -> np.ndarray:
+    """Host float64 filter from the library's own construction (no GPU needed)."""
+    out = np.zeros(size, np.float64)
+    check(load().wst_host_filter(M, N, J, L, kind, j, l, r,
+                                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), size))
+    return out
+
+
+class Plan:
+    """Owning handle of a ``wst_plan`` (bound to the device current at creation)."""
+
+    def __init__(self, M, N, J, L, max_order=2, pre_pad=False):
+        lib = load()
+        h = ctypes.c_void_p()
+        check(lib.wst_plan_create(int(M), int(N), int(J), int(L), int(max_order),
+                                  1 if pre_pad else 0, ctypes.byref(h)))
+        self._h = h
+        K, Mo, No = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(lib.wst_output_shape(h, ctypes.byref(K), ctypes.byref(Mo), ctypes.byref(No)))
+        self.K, self.Mo, self.No = K.value, Mo.value, No.value
+        PM, PN = ctypes.c_int(), ctypes.c_int()
+        check(lib.wst_padded_shape(h, ctypes.byref(PM), ctypes.byref(PN)))
+        self.PM, self.PN = PM.value, PN.value
+
+    @property
+    def handle(self):
+        return self._h
+
+    def workspace_bytes(self, nbatch: int) -> int:
+        b = ctypes.c_size_t()
+        check(load().wst_workspace_bytes(self._h, int(nbatch), ctypes.byref(b)))
+        return b.value
+
+    def forward(self, d_in: int, nbatch: int, d_out: int, pooled: bool, d_ws: int, ws_bytes: int,
+                stream: int) -> None:
+        check(load().wst_forward(self._h, ctypes.c_void_p(d_in), int(nbatch),
+                                 ctypes.c_void_p(d_out), 1 if pooled else 0,
+                                 ctypes.c_void_p(d_ws or None), int(ws_bytes),
+                                 ctypes.c_void_p(stream or None)))
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and _lib is not None:
+            _lib.wst_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,699 @@
+// MI355X (gfx950) wavelet scattering transform: kernels + C ABI (include/wst_hip.h).
+//
+// Replaces kymatio 0.3.0's scattering2d cascade as reached from the
+// reference at src/training/train_and_save_model.py:359-376 and src/inference/inference.py:242-257.
+//
+// Pipeline per chunk of planes (one plane = one channel of one patch):
+//   k_prep     (1 workgroup / plane):  reflect-pad gather -> S0 (separable spatial low-pass) ->
+//                                       mean-centred forward 2-D DFT -> Xhat (HBM workspace)
+//   k_order12  (1 workgroup / (plane, theta1), one launch per j1):
+//                                       fold(Xhat * psi0) -> inverse DFT -> |.| -> S1 low-pass;
+//                                       forward DFT of U1 kept in LDS -> for every (j2 > j1, theta2)
+//                                       fold(U1hat * psi) -> inverse DFT -> |.| -> S2 low-pass.
+// All per-path intermediates stay in LDS; HBM sees the input plane, Xhat (written once, re-read
+// by the L workgroups of the plane on the same XCD) and the K output coefficients.
+//
+// Exact rewrites used (identities of the kymatio algorithm, not approximations):
+//   * sub(Y, k) then ifft at n/k   ==  ifft at n then spatial decimation by k;
+//   * the phi low-pass + subsample + ifft + unpad == a separable spatial filter evaluated only at
+//     the (Mo x No) kept points (phi_hat levels are outer products of 1-D masked crops);
+//   * constants are removed before the psi paths (psi_hat(0) ~ 1e-16, reflect padding preserves
+//     constants), which conditions the fp32 band-pass content.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "filter_bank.h"
+#include "wst_hip.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define WST_HIP_CHECK(expr)                                                                   \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(WST_ERR_HIP, std::string(#expr " failed: ") + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr int kMaxLds = 160 * 1024;
+constexpr int kMaxO = 8;  // outputs per thread per DFT chunk (register tile)
+
+// Kernel-side description of a plan (POD, passed by value).
+struct DevParams {
+    int M, N, PM, PN, J, L, max_order, pre_pad, K;
+    int mM, mN, oM, oN, padTop, padLeft;
+    int tw_total, lp_total;       // element counts of the twiddle / low-pass pools
+    const float* psi;             // concatenated psi Fourier levels (fp32)
+    const long long* psi_off;     // [(j*L + l)*J + r]
+    const float* lp;              // concatenated spatial low-pass taps hM[r], hN[r]
+    const int* lp_off;            // [2r] -> hM[r], [2r+1] -> hN[r]
+    const float2* tw;             // concatenated twiddle tables exp(-2 pi i k / n)
+    const int* tw_off;            // [2r] -> n = PM>>r, [2r+1] -> n = PN>>r, r in [0, J]
+    const int* o2_base;           // first order-2 coefficient of each n1 = j1*L + l1
+};
+
+// ------------------------------------------------------------------------------------------
+// device helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int reflect_index(int i, int n) {
+    // numpy.pad(mode='reflect') for any pad width: even periodic extension, period 2(n-1)
+    if (n == 1) return 0;
+    const int period = 2 * (n - 1);
+    int t = i % period;
+    if (t < 0) t += period;
+    return t < n ? t : period - t;
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    float s = 0.f;
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int w = 0; w < nw; ++w) s += red[w];
+    return s;
+}
+
+// Batched in-place DFT along one axis.  Array b, line l, element e lives at
+// base[b*bs + l*ls + e*es].  Lines are processed in chunks of whole lines that fit the register
+// tile (T * kMaxO outputs): read phase -> barrier -> write phase.  Ends with a barrier.
+__device__ void lds_dft_lines(float2* base, int nb, int bs, int nl, int ls, int es, int n,
+                              const float2* tw, bool inverse) {
+    const int T = blockDim.x;
+    const int lines_total = nb * nl;
+    int lpc = (T * kMaxO) / n;
+    if (lpc < 1) lpc = 1;
+    const float sgn = inverse ? -1.f : 1.f;
+    for (int l0 = 0; l0 < lines_total; l0 += lpc) {
+        const int nlc = min(lpc, lines_total - l0);
+        const int nout = nlc * n;
+        float2 acc[kMaxO];
+        int addr[kMaxO];
+#pragma unroll
+        for (int i = 0; i < kMaxO; ++i) {
+            const int o = threadIdx.x + i * T;
+            addr[i] = -1;
+            acc[i] = make_float2(0.f, 0.f);
+            if (o < nout) {
+                const int lc = o / n;
+                const int k = o - lc * n;
+                const int Lg = l0 + lc;
+                const int b = Lg / nl;
+                const int l = Lg - b * nl;
+                const float2* src = base + b * bs + l * ls;
+                float sr = 0.f, si = 0.f;
+                int idx = 0;
+                for (int e = 0; e < n; ++e) {
+                    const float2 x = src[e * es];
+                    const float2 w = tw[idx];
+                    const float wy = sgn * w.y;
+                    sr = fmaf(x.x, w.x, fmaf(-x.y, wy, sr));
+                    si = fmaf(x.x, wy, fmaf(x.y, w.x, si));
+                    idx += k;
+                    if (idx >= n) idx -= n;
+                }
+                acc[i] = make_float2(sr, si);
+                addr[i] = b * bs + l * ls + k * es;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kMaxO; ++i)
+            if (addr[i] >= 0) base[addr[i]] = acc[i];
+    }
+    __syncthreads();
+}
+
+// 2-D DFT (rows x cols, row stride cols) of nb arrays spaced bs apart.
+__device__ void lds_dft2(float2* buf, int nb, int bs, int rows, int cols, const float2* twR,
+                         const float2* twC, bool inverse) {
+    lds_dft_lines(buf, nb, bs, rows, cols, 1, cols, twC, inverse);  // along columns index
+    lds_dft_lines(buf, nb, bs, cols, 1, cols, rows, twR, inverse);  // along rows index
+}
+
+// Separable phi low-pass evaluated at the kept output points (unpad folded in):
+//   S[b][a][c] = sum_p hM[(s(a+1) - p) mod rows] * sum_q hN[(s(c+1) - q) mod cols] * U[b][p][q]
+// U real (stored in .x).  tmp: nb*rows*oN floats, S: nb*oM*oN floats.  Ends with a barrier.
+__device__ void lds_lowpass(const float2* U, int nb, int bs, int rows, int cols, const float* hM,
+                            const float* hN, int s, int oM, int oN, float* tmp, float* S) {
+    const int T = blockDim.x;
+    const int tot1 = nb * rows * oN;
+    for (int o = threadIdx.x; o < tot1; o += T) {
+        const int c = o % oN;
+        const int p = (o / oN) % rows;
+        const int b = o / (oN * rows);
+        const float2* row = U + b * bs + p * cols;
+        int idx = s * (c + 1);
+        float acc = 0.f;
+        for (int q = 0; q < cols; ++q) {
+            acc = fmaf(row[q].x, hN[idx], acc);
+            idx = (idx == 0) ? cols - 1 : idx - 1;
+        }
+        tmp[o] = acc;
+    }
+    __syncthreads();
+    const int tot2 = nb * oM * oN;
+    for (int o = threadIdx.x; o < tot2; o += T) {
+        const int c = o % oN;
+        const int a = (o / oN) % oM;
+        const int b = o / (oN * oM);
+        const float* t = tmp + b * rows * oN + c;
+        int idx = s * (a + 1);
+        float acc = 0.f;
+        for (int p = 0; p < rows; ++p) {
+            acc = fmaf(hM[idx], t[p * oN], acc);
+            idx = (idx == 0) ? rows - 1 : idx - 1;
+        }
+        S[o] = acc;
+    }
+    __syncthreads();
+}
+
+// Write nb coefficient maps (S: nb x oM x oN) of plane `img`, coefficient k0 + b.
+// pooled: out[img][k] = mean, out[img][K + k] = population std.
+__device__ void emit(const float* S, int nb, int k0, int kstride, long long img, int K, int oM,
+                     int oN, float* out, int pooled) {
+    const int npix = oM * oN;
+    if (!pooled) {
+        const int tot = nb * npix;
+        for (int o = threadIdx.x; o < tot; o += blockDim.x) {
+            const int b = o / npix;
+            const int k = k0 + b * kstride;
+            out[(img * K + k) * npix + (o - b * npix)] = S[o];
+        }
+    } else {
+        for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+            const float* v = S + b * npix;
+            float m = 0.f;
+            for (int i = 0; i < npix; ++i) m += v[i];
+            m /= npix;
+            float q = 0.f;
+            for (int i = 0; i < npix; ++i) {
+                const float d = v[i] - m;
+                q = fmaf(d, d, q);
+            }
+            const int k = k0 + b * kstride;
+            out[img * 2 * K + k] = m;
+            out[img * 2 * K + K + k] = sqrtf(q / npix);
+        }
+    }
+}
+
+// Copy the twiddle and low-pass pools into LDS.
+__device__ void load_tables(const DevParams& p, float2* tw_l, float* lp_l) {
+    for (int i = threadIdx.x; i < p.tw_total; i += blockDim.x) tw_l[i] = p.tw[i];
+    for (int i = threadIdx.x; i < p.lp_total; i += blockDim.x) lp_l[i] = p.lp[i];
+}
+
+// ------------------------------------------------------------------------------------------
+// k_prep: one workgroup per plane
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(512) k_prep(DevParams p, const float* __restrict__ in,
+                                              long long img0, float2* __restrict__ xhat,
+                                              float* __restrict__ out, int pooled) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int PM = p.PM, PN = p.PN, n = PM * PN;
+    float2* A = reinterpret_cast<float2*>(smem);
+    float2* tw_l = A + n;
+    float* lp_l = reinterpret_cast<float*>(tw_l + p.tw_total);
+    float* tmp = lp_l + p.lp_total;                 // PM * oN
+    float* S = tmp + PM * p.oN;                     // oM * oN
+    float* red = S + p.oM * p.oN;                   // 16
+
+    const long long local = blockIdx.x;
+    const long long img = img0 + local;
+    load_tables(p, tw_l, lp_l);
+    const int inM = p.pre_pad ? PM : p.M, inN = p.pre_pad ? PN : p.N;
+    const float* x = in + local * inM * inN;
+    float part = 0.f;
+    for (int o = threadIdx.x; o < n; o += blockDim.x) {
+        const int u = o / PN, v = o - (o / PN) * PN;
+        int su, sv;
+        if (p.pre_pad) {
+            su = u;
+            sv = v;
+        } else {
+            su = reflect_index(u - p.padTop, p.M);
+            sv = reflect_index(v - p.padLeft, p.N);
+        }
+        const float val = x[su * inN + sv];
+        A[o] = make_float2(val, 0.f);
+        part += val;
+    }
+    const float mean = block_sum(part, red) / n;  // contains the barrier after the gather
+
+    // S0: low-pass at level 0, decimation 2^J
+    lds_lowpass(A, 1, 0, PM, PN, lp_l + p.lp_off[0], lp_l + p.lp_off[1], 1 << p.J, p.oM, p.oN,
+                tmp, S);
+    emit(S, 1, 0, 1, img, p.K, p.oM, p.oN, out, pooled);
+
+    // mean-centred forward DFT for the band-pass paths
+    for (int o = threadIdx.x; o < n; o += blockDim.x) A[o].x -= mean;
+    __syncthreads();
+    lds_dft2(A, 1, 0, PM, PN, tw_l + p.tw_off[0], tw_l + p.tw_off[1], false);
+    float2* dst = xhat + local * n;
+    for (int o = threadIdx.x; o < n; o += blockDim.x) dst[o] = A[o];
+}
+
+// ------------------------------------------------------------------------------------------
+// k_order12: one workgroup per (plane, theta1) at fixed j1
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int nimg,
+                                                 long long img0, const float2* __restrict__ xhat,
+                                                 float* __restrict__ out, int pooled) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int J = p.J, L = p.L;
+    // XCD-aware decode: blocks b and b+8 share an XCD; give each XCD a contiguous range of
+    // (plane, theta1) items so a plane's L workgroups re-read its Xhat from one L2.
+    const int total = nimg * L;
+    int item = blockIdx.x;
+    if ((total & 7) == 0) item = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+    const int local = item / L;
+    const int l1 = item - local * L;
+    const long long img = img0 + local;
+
+    const int PM = p.PM, PN = p.PN;
+    const int nM1 = PM >> j1, nN1 = PN >> j1, n1 = nM1 * nN1;
+    const bool do2 = (p.max_order >= 2) && (j1 < J - 1);
+    const int nM2max = nM1 >> 1, nN2max = nN1 >> 1;
+    const int slot = do2 ? nM2max * nN2max : 0;
+
+    float2* A = reinterpret_cast<float2*>(smem);
+    float2* B = A + n1;
+    float2* tw_l = B + G * slot;
+    float* lp_l = reinterpret_cast<float*>(tw_l + p.tw_total);
+    float* tmp = lp_l + p.lp_total;                   // G * nM1 * oN
+    float* S = tmp + G * nM1 * p.oN;                  // G * oM * oN
+    float* red = S + G * p.oM * p.oN;                 // 16
+
+    load_tables(p, tw_l, lp_l);
+
+    // 1. fold_{2^j1}(Xhat * psi0_{j1,l1}) straight from HBM/L2
+    const float* psi0 = p.psi + p.psi_off[(j1 * L + l1) * J + 0];
+    const float2* X = xhat + static_cast<long long>(local) * PM * PN;
+    const int s1 = 1 << j1;
+    for (int o = threadIdx.x; o < n1; o += blockDim.x) {
+        const int u = o / nN1, v = o - (o / nN1) * nN1;
+        float ar = 0.f, ai = 0.f;
+        for (int i = 0; i < s1; ++i) {
+            const int rowoff = (u + i * nM1) * PN + v;
+            for (int j = 0; j < s1; ++j) {
+                const int idx = rowoff + j * nN1;
+                const float f = psi0[idx];
+                const float2 xv = X[idx];
+                ar = fmaf(xv.x, f, ar);
+                ai = fmaf(xv.y, f, ai);
+            }
+        }
+        A[o] = make_float2(ar, ai);
+    }
+    __syncthreads();
+
+    // 2. U1 = |ifft(.)| ; combined normalisation of fold-mean and ifft = 1 / (PM * PN)
+    lds_dft2(A, 1, 0, nM1, nN1, tw_l + p.tw_off[2 * j1], tw_l + p.tw_off[2 * j1 + 1], true);
+    const float sc1 = 1.f / (static_cast<float>(PM) * static_cast<float>(PN));
+    float part = 0.f;
+    for (int o = threadIdx.x; o < n1; o += blockDim.x) {
+        const float2 z = A[o];
+        const float m = sqrtf(z.x * z.x + z.y * z.y) * sc1;
+        A[o] = make_float2(m, 0.f);
+        part += m;
+    }
+    const float mean1 = block_sum(part, red) / n1;
+
+    // 3. S1 at level j1, decimation 2^(J-j1)
+    lds_lowpass(A, 1, 0, nM1, nN1, lp_l + p.lp_off[2 * j1], lp_l + p.lp_off[2 * j1 + 1],
+                1 << (J - j1), p.oM, p.oN, tmp, S);
+    const int n1idx = j1 * L + l1;
+    emit(S, 1, 1 + n1idx, 1, img, p.K, p.oM, p.oN, out, pooled);
+    if (!do2) return;
+
+    // 4. U1hat = fft(U1 - mean) kept in LDS
+    for (int o = threadIdx.x; o < n1; o += blockDim.x) A[o].x -= mean1;
+    __syncthreads();
+    lds_dft2(A, 1, 0, nM1, nN1, tw_l + p.tw_off[2 * j1], tw_l + p.tw_off[2 * j1 + 1], false);
+
+    const float sc2 = 1.f / static_cast<float>(n1);
+    const int kbase = p.o2_base[n1idx];
+    for (int j2 = j1 + 1; j2 < J; ++j2) {
+        const int nM2 = PM >> j2, nN2 = PN >> j2, n2 = nM2 * nN2;
+        const int s2 = 1 << (j2 - j1);
+        for (int l2a = 0; l2a < L; l2a += G) {
+            const int g = min(G, L - l2a);
+            // fold_{2^(j2-j1)}(U1hat * psi^{j1}_{j2,l2})
+            for (int o = threadIdx.x; o < g * n2; o += blockDim.x) {
+                const int b = o / n2;
+                const int r = o - b * n2;
+                const int u = r / nN2, v = r - (r / nN2) * nN2;
+                const float* ps = p.psi + p.psi_off[(j2 * L + l2a + b) * J + j1];
+                float ar = 0.f, ai = 0.f;
+                for (int i = 0; i < s2; ++i) {
+                    const int rowoff = (u + i * nM2) * nN1 + v;
+                    for (int j = 0; j < s2; ++j) {
+                        const int idx = rowoff + j * nN2;
+                        const float f = ps[idx];
+                        const float2 xv = A[idx];
+                        ar = fmaf(xv.x, f, ar);
+                        ai = fmaf(xv.y, f, ai);
+                    }
+                }
+                B[b * slot + r] = make_float2(ar, ai);
+            }
+            __syncthreads();
+            lds_dft2(B, g, slot, nM2, nN2, tw_l + p.tw_off[2 * j2], tw_l + p.tw_off[2 * j2 + 1],
+                     true);
+            for (int o = threadIdx.x; o < g * n2; o += blockDim.x) {
+                const int b = o / n2;
+                const int r = o - b * n2;
+                const float2 z = B[b * slot + r];
+                B[b * slot + r] = make_float2(sqrtf(z.x * z.x + z.y * z.y) * sc2, 0.f);
+            }
+            __syncthreads();
+            lds_lowpass(B, g, slot, nM2, nN2, lp_l + p.lp_off[2 * j2], lp_l + p.lp_off[2 * j2 + 1],
+                        1 << (J - j2), p.oM, p.oN, tmp, S);
+            emit(S, g, kbase + (j2 - j1 - 1) * L + l2a, 1, img, p.K, p.oM, p.oN, out, pooled);
+            __syncthreads();
+        }
+    }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// plan
+// ------------------------------------------------------------------------------------------
+struct wst_plan {
+    wst::Geometry g;
+    int device = 0;
+    DevParams dp{};
+    // device allocations
+    float* d_psi = nullptr;
+    long long* d_psi_off = nullptr;
+    float* d_lp = nullptr;
+    int* d_lp_off = nullptr;
+    float2* d_tw = nullptr;
+    int* d_tw_off = nullptr;
+    int* d_o2 = nullptr;
+    // launch geometry
+    int prep_threads = 256;
+    size_t prep_lds = 0;
+    std::vector<int> k1_threads, k1_G;
+    std::vector<size_t> k1_lds;
+    // internal workspace (used when the caller passes none)
+    mutable std::mutex ws_mu;
+    mutable void* ws = nullptr;
+    mutable size_t ws_bytes = 0;
+    std::vector<int> lp_off_h, tw_off_h;
+};
+
+namespace {
+
+void free_plan(wst_plan* p) {
+    if (!p) return;
+    (void)hipFree(p->d_psi);
+    (void)hipFree(p->d_psi_off);
+    (void)hipFree(p->d_lp);
+    (void)hipFree(p->d_lp_off);
+    (void)hipFree(p->d_tw);
+    (void)hipFree(p->d_tw_off);
+    (void)hipFree(p->d_o2);
+    if (p->ws) (void)hipFree(p->ws);
+    delete p;
+}
+
+template <typename T>
+int upload(T** dst, const std::vector<T>& src) {
+    const size_t bytes = std::max<size_t>(1, src.size()) * sizeof(T);
+    WST_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(dst), bytes));
+    if (!src.empty()) WST_HIP_CHECK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+    return WST_OK;
+}
+
+size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
+
+}  // namespace
+
+extern "C" {
+
+int wst_abi_version(void) { return WST_ABI_VERSION; }
+
+const char* wst_last_error(void) { return g_last_error.c_str(); }
+
+int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_plan** out) {
+    if (!out) return fail(WST_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    if (J < 1) return fail(WST_ERR_INVALID, "J must be >= 1 (kymatio needs phi level 0)");
+    wst::Geometry g;
+    std::string err;
+    if (!wst::make_geometry(M, N, J, L, max_order, g, err)) return fail(WST_ERR_INVALID, err);
+    wst::FilterBank fb;
+    try {
+        fb = wst::build_filter_bank(g);
+    } catch (const std::exception& e) {
+        return fail(WST_ERR_UNSUPPORTED, e.what());
+    }
+
+    std::unique_ptr<wst_plan, void (*)(wst_plan*)> plan(new (std::nothrow) wst_plan(), free_plan);
+    if (!plan) return fail(WST_ERR_NOMEM, "host allocation failed");
+    plan->g = g;
+    WST_HIP_CHECK(hipGetDevice(&plan->device));
+
+    // --- flatten filters ---
+    std::vector<float> psi;
+    std::vector<long long> psi_off(static_cast<size_t>(J) * L * J, -1);
+    for (int j = 0; j < J; ++j)
+        for (int l = 0; l < L; ++l) {
+            const auto& lev = fb.psi[static_cast<size_t>(j) * L + l];
+            for (int r = 0; r < static_cast<int>(lev.size()); ++r) {
+                psi_off[(static_cast<size_t>(j) * L + l) * J + r] = static_cast<long long>(psi.size());
+                for (double v : lev[r]) psi.push_back(static_cast<float>(v));
+            }
+        }
+    std::vector<float> lp;
+    std::vector<int> lp_off(2 * static_cast<size_t>(J));
+    for (int r = 0; r < J; ++r) {
+        lp_off[2 * r] = static_cast<int>(lp.size());
+        for (double v : fb.hM[r]) lp.push_back(static_cast<float>(v));
+        lp_off[2 * r + 1] = static_cast<int>(lp.size());
+        for (double v : fb.hN[r]) lp.push_back(static_cast<float>(v));
+    }
+    std::vector<float2> tw;
+    std::vector<int> tw_off(2 * static_cast<size_t>(J + 1));
+    for (int r = 0; r <= J; ++r)
+        for (int d = 0; d < 2; ++d) {
+            const int n = (d == 0 ? g.PM : g.PN) >> r;
+            tw_off[2 * r + d] = static_cast<int>(tw.size());
+            for (int k = 0; k < n; ++k) {
+                const double a = 2.0 * 3.14159265358979323846 * k / n;
+                tw.push_back(make_float2(static_cast<float>(std::cos(a)), static_cast<float>(-std::sin(a))));
+            }
+        }
+    std::vector<int> o2(static_cast<size_t>(J) * L, 0);
+    {
+        int k = 1 + J * L;
+        for (int j1 = 0; j1 < J; ++j1)
+            for (int l1 = 0; l1 < L; ++l1) {
+                o2[static_cast<size_t>(j1) * L + l1] = k;
+                if (max_order >= 2) k += L * (J - 1 - j1);
+            }
+    }
+
+    int rc;
+    if ((rc = upload(&plan->d_psi, psi)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_psi_off, psi_off)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_lp, lp)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_lp_off, lp_off)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_tw, tw)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_tw_off, tw_off)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_o2, o2)) != WST_OK) return rc;
+    plan->lp_off_h = lp_off;
+    plan->tw_off_h = tw_off;
+
+    DevParams& dp = plan->dp;
+    dp.M = g.M; dp.N = g.N; dp.PM = g.PM; dp.PN = g.PN; dp.J = J; dp.L = L;
+    dp.max_order = max_order; dp.pre_pad = pre_pad ? 1 : 0; dp.K = g.K;
+    dp.mM = g.mM; dp.mN = g.mN; dp.oM = g.oM; dp.oN = g.oN;
+    dp.padTop = g.padTop; dp.padLeft = g.padLeft;
+    dp.tw_total = static_cast<int>(tw.size());
+    dp.lp_total = static_cast<int>(lp.size());
+    dp.psi = plan->d_psi; dp.psi_off = plan->d_psi_off;
+    dp.lp = plan->d_lp; dp.lp_off = plan->d_lp_off;
+    dp.tw = plan->d_tw; dp.tw_off = plan->d_tw_off;
+    dp.o2_base = plan->d_o2;
+
+    // --- LDS budgets ---
+    const size_t tables = align16(tw.size() * sizeof(float2)) + align16(lp.size() * sizeof(float));
+    const size_t P2 = static_cast<size_t>(g.PM) * g.PN;
+    plan->prep_lds = align16(P2 * sizeof(float2)) + tables +
+                     align16((static_cast<size_t>(g.PM) * g.oN + g.oM * g.oN + 16) * sizeof(float));
+    if (plan->prep_lds > static_cast<size_t>(kMaxLds))
+        return fail(WST_ERR_UNSUPPORTED,
+                    "padded plane " + std::to_string(g.PM) + "x" + std::to_string(g.PN) +
+                        " exceeds the LDS-resident path (160 KiB per CU)");
+    plan->prep_threads = P2 >= 4096 ? 512 : 256;
+    plan->k1_threads.resize(J);
+    plan->k1_G.resize(J);
+    plan->k1_lds.resize(J);
+    for (int j1 = 0; j1 < J; ++j1) {
+        const size_t n1 = static_cast<size_t>(g.PM >> j1) * (g.PN >> j1);
+        const bool do2 = max_order >= 2 && j1 < J - 1;
+        const size_t slot = do2 ? static_cast<size_t>(g.PM >> (j1 + 1)) * (g.PN >> (j1 + 1)) : 0;
+        auto lds_for = [&](int G) {
+            return align16(n1 * sizeof(float2)) + align16(G * slot * sizeof(float2)) + tables +
+                   align16((static_cast<size_t>(G) * (g.PM >> j1) * g.oN +
+                            static_cast<size_t>(G) * g.oM * g.oN + 16) * sizeof(float));
+        };
+        int G = do2 ? std::min(L, 8) : 1;
+        while (G > 1 && lds_for(G) > static_cast<size_t>(kMaxLds)) --G;
+        if (lds_for(G) > static_cast<size_t>(kMaxLds))
+            return fail(WST_ERR_UNSUPPORTED, "order-1 plane at j1=" + std::to_string(j1) +
+                                                 " exceeds the LDS-resident path (160 KiB per CU)");
+        plan->k1_G[j1] = G;
+        plan->k1_lds[j1] = lds_for(G);
+        plan->k1_threads[j1] = n1 >= 4096 ? 512 : 256;
+    }
+    WST_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_prep),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));
+    WST_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_order12),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));
+    *out = plan.release();
+    g_last_error.clear();
+    return WST_OK;
+}
+
+int wst_plan_destroy(wst_plan* plan) {
+    free_plan(plan);
+    return WST_OK;
+}
+
+int wst_output_shape(const wst_plan* plan, int* K, int* Mo, int* No) {
+    if (!plan) return fail(WST_ERR_INVALID, "plan is NULL");
+    if (K) *K = plan->g.K;
+    if (Mo) *Mo = plan->g.oM;
+    if (No) *No = plan->g.oN;
+    return WST_OK;
+}
+
+int wst_padded_shape(const wst_plan* plan, int* PM, int* PN) {
+    if (!plan) return fail(WST_ERR_INVALID, "plan is NULL");
+    if (PM) *PM = plan->g.PM;
+    if (PN) *PN = plan->g.PN;
+    return WST_OK;
+}
+
+int wst_workspace_bytes(const wst_plan* plan, int64_t nbatch, size_t* bytes) {
+    if (!plan || !bytes) return fail(WST_ERR_INVALID, "plan/bytes is NULL");
+    if (nbatch < 0) return fail(WST_ERR_INVALID, "nbatch < 0");
+    *bytes = static_cast<size_t>(nbatch) * plan->g.PM * plan->g.PN * sizeof(float2);
+    return WST_OK;
+}
+
+int wst_forward(const wst_plan* plan, const float* d_in, int64_t nbatch, float* d_out, int pooled,
+                void* d_workspace, size_t workspace_bytes, void* stream_) {
+    if (!plan) return fail(WST_ERR_INVALID, "plan is NULL");
+    if (nbatch < 0) return fail(WST_ERR_INVALID, "nbatch < 0");
+    if (nbatch == 0) return WST_OK;
+    if (!d_in || !d_out) return fail(WST_ERR_INVALID, "input/output pointer is NULL");
+    int dev = -1;
+    WST_HIP_CHECK(hipGetDevice(&dev));
+    if (dev != plan->device)
+        return fail(WST_ERR_HIP, "plan was created on device " + std::to_string(plan->device) +
+                                     " but device " + std::to_string(dev) + " is current");
+    hipStream_t stream = reinterpret_cast<hipStream_t>(stream_);
+    const wst::Geometry& g = plan->g;
+    const size_t plane_ws = static_cast<size_t>(g.PM) * g.PN * sizeof(float2);
+    void* ws = d_workspace;
+    size_t wsb = workspace_bytes;
+    if (!ws) {
+        // internal workspace: up to 2048 planes per chunk (Xhat chunk stays MALL-resident)
+        const int64_t want = std::min<int64_t>(nbatch, 2048);
+        std::lock_guard<std::mutex> lk(plan->ws_mu);
+        if (plan->ws_bytes < want * plane_ws) {
+            if (plan->ws) {
+                WST_HIP_CHECK(hipStreamSynchronize(stream));
+                (void)hipFree(plan->ws);
+                plan->ws = nullptr;
+                plan->ws_bytes = 0;
+            }
+            WST_HIP_CHECK(hipMalloc(&plan->ws, want * plane_ws));
+            plan->ws_bytes = want * plane_ws;
+        }
+        ws = plan->ws;
+        wsb = plan->ws_bytes;
+    }
+    const int64_t chunk = static_cast<int64_t>(wsb / plane_ws);
+    if (chunk < 1) return fail(WST_ERR_INVALID, "workspace smaller than one padded plane");
+    const int inM = plan->dp.pre_pad ? g.PM : g.M, inN = plan->dp.pre_pad ? g.PN : g.N;
+    float2* xhat = reinterpret_cast<float2*>(ws);
+    for (int64_t c0 = 0; c0 < nbatch; c0 += chunk) {
+        const int nimg = static_cast<int>(std::min<int64_t>(chunk, nbatch - c0));
+        hipLaunchKernelGGL(k_prep, dim3(nimg), dim3(plan->prep_threads), plan->prep_lds, stream,
+                           plan->dp, d_in + c0 * inM * inN, static_cast<long long>(c0), xhat, d_out,
+                           pooled);
+        WST_HIP_CHECK(hipGetLastError());
+        for (int j1 = 0; j1 < g.J; ++j1) {
+            hipLaunchKernelGGL(k_order12, dim3(nimg * g.L), dim3(plan->k1_threads[j1]),
+                               plan->k1_lds[j1], stream, plan->dp, j1, plan->k1_G[j1], nimg,
+                               static_cast<long long>(c0), xhat, d_out, pooled);
+            WST_HIP_CHECK(hipGetLastError());
+        }
+    }
+    return WST_OK;
+}
+
+int wst_host_filter(int M, int N, int J, int L, int kind, int j, int l, int r, double* out,
+                    int64_t len) {
+    if (!out) return fail(WST_ERR_INVALID, "out is NULL");
+    if (J < 1) return fail(WST_ERR_INVALID, "J must be >= 1");
+    wst::Geometry g;
+    std::string err;
+    if (!wst::make_geometry(M, N, J, L, 2, g, err)) return fail(WST_ERR_INVALID, err);
+    try {
+        wst::FilterBank fb = wst::build_filter_bank(g);
+        std::vector<double> v;
+        if (kind == 0) {
+            if (j < 0 || j >= J || l < 0 || l >= L) return fail(WST_ERR_INVALID, "bad (j, l)");
+            const auto& lev = fb.psi[static_cast<size_t>(j) * L + l];
+            if (r < 0 || r >= static_cast<int>(lev.size())) return fail(WST_ERR_INVALID, "bad level");
+            v = lev[r];
+        } else if (kind >= 1 && kind <= 3) {
+            if (r < 0 || r >= J) return fail(WST_ERR_INVALID, "bad level");
+            if (kind == 1) {
+                const auto& a = fb.aM[r];
+                const auto& b = fb.aN[r];
+                v.resize(a.size() * b.size());
+                for (size_t i = 0; i < a.size(); ++i)
+                    for (size_t k = 0; k < b.size(); ++k) v[i * b.size() + k] = a[i] * b[k];
+            } else {
+                v = (kind == 2) ? fb.hM[r] : fb.hN[r];
+            }
+        } else {
+            return fail(WST_ERR_INVALID, "bad kind");
+        }
+        if (static_cast<int64_t>(v.size()) > len) return fail(WST_ERR_INVALID, "output buffer too small");
+        std::memcpy(out, v.data(), v.size() * sizeof(double));
+    } catch (const std::exception& e) {
+        return fail(WST_ERR_UNSUPPORTED, e.what());
+    }
+    return WST_OK;
+}
+
+}  // extern "C"

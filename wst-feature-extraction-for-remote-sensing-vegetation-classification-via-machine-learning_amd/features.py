@@ -1,0 +1,73 @@
+"""WST feature layouts of the reference's callers (row F1 of SURVEY.md §8(f)).
+
+* Training layout -- src/training/train_and_save_model.py:346-378: per channel
+  ``[mean_k (K) | std_k (K)]`` (population std over the (Mo, No) map), channels concatenated:
+  C * 2K features (486 for RGB at J=2, L=8).  Names follow get_feature_names :400-427, with
+  the hard-coded 81 replaced by the true K for any (J, L).
+* Inference layout -- src/inference/inference.py:237-270: per channel interleaved
+  ``[m_0, s_0, m_1, s_1, ...]``.
+
+The pooling is fused into the HIP kernels' epilogue (pooled=1): only 2K floats per plane leave
+the GPU instead of K*Mo*No.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .frontend import require_gpu, scatter_device, num_coefficients
+
+CHANNEL_NAMES = ("R", "G", "B")
+
+
+def get_feature_names(J: int = 2, L: int = 8, channels=CHANNEL_NAMES, max_order: int = 2):
+    """``{ch}_wst_{mean|std}_{k}`` in training order (channel -> stat -> k)."""
+    K = num_coefficients(J, L, max_order)
+    return [f"{c}_wst_{s}_{i}" for c in channels for s in ("mean", "std") for i in range(K)]
+
+
+def _pooled_batch(images, J, L, max_order):
+    """images: (B, C, H, W) numpy or torch -> torch (B, C, 2K) float32 on the GPU."""
+    import torch
+    require_gpu()
+    if isinstance(images, np.ndarray):
+        x = torch.from_numpy(np.ascontiguousarray(images, dtype=np.float32)).to("cuda")
+    else:
+        x = images.detach().to(device="cuda" if not images.is_cuda else images.device,
+                                dtype=torch.float32).contiguous()
+    if x.dim() != 4:
+        raise RuntimeError("images must be (B, C, H, W)")
+    B, C, H, W = x.shape
+    F = scatter_device(x.reshape(B * C, H, W), H, W, J, L, max_order, False, pooled=True)
+    return F.reshape(B, C, -1)
+
+
+def extract_wst_features_batch(images, J: int = 2, L: int = 8, max_order: int = 2,
+                               as_numpy: bool = True):
+    """Training-layout features for a batch: (B, C, H, W) -> (B, C*2K).
+
+    One GPU call replaces the reference's B*C serial kymatio calls
+    (train_and_save_model.py:486-488 x :364-376)."""
+    F = _pooled_batch(images, J, L, max_order)
+    F = F.reshape(F.shape[0], -1)
+    return F.cpu().numpy().astype(np.float64) if as_numpy else F
+
+
+def extract_wst_features(rgb_image, J: int = 2, L: int = 8):
+    """Drop-in for train_and_save_model.py:346-378 ``extract_wst_features(rgb_image)``:
+    (C, H, W) float -> (C*2K,) float64."""
+    return extract_wst_features_batch(np.asarray(rgb_image)[None], J, L)[0]
+
+
+def extract_wst_features_interleaved_batch(images, J: int = 2, L: int = 8, max_order: int = 2,
+                                           as_numpy: bool = True):
+    """Inference layout (inference.py:263-266): per channel [m_0, s_0, m_1, s_1, ...]."""
+    F = _pooled_batch(images, J, L, max_order)          # (B, C, 2K) = [means | stds]
+    B, C, K2 = F.shape
+    K = K2 // 2
+    inter = F.reshape(B, C, 2, K).transpose(2, 3).reshape(B, C * 2 * K)
+    return inter.cpu().numpy().astype(np.float64) if as_numpy else inter
+
+
+def extract_wst_features_interleaved(rgb_image, J: int = 2, L: int = 8):
+    """Drop-in for inference.py:237-270 ``ModelInference.extract_wst_features``."""
+    return extract_wst_features_interleaved_batch(np.asarray(rgb_image)[None], J, L)[0]

@@ -1,0 +1,49 @@
+"""NumPy frontend: drop-in for ``from kymatio.numpy import Scattering2D``.
+
+Reference call sites: src/training/train_and_save_model.py:46,359,368 and
+src/visualization/visualize_features.py:30.  The array is staged to the GPU (H2D), transformed
+by the HIP library, and copied back (D2H).  Output dtype is float32 (the compute precision).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .frontend import ScatteringBase2D, require_gpu, scatter_device
+
+
+class Scattering2D(ScatteringBase2D):
+    """Scattering2D(J, shape, L=8, max_order=2, pre_pad=False, backend=None, out_type='array')."""
+
+    def scattering(self, input):
+        if not isinstance(input, np.ndarray):
+            raise TypeError("The input should be a NumPy array.")
+        if np.iscomplexobj(input):
+            raise TypeError("The input should be real.")
+        self._check_spatial(input.shape, "array")
+        require_gpu()
+        import torch
+        batch_shape = input.shape[:-2]
+        x = np.ascontiguousarray(input, dtype=np.float32).reshape((-1,) + input.shape[-2:])
+        xd = torch.from_numpy(x).to("cuda", non_blocking=False)
+        S = scatter_device(xd, self.M, self.N, self.J, self.L, self.max_order, self.pre_pad)
+        S = S.cpu().numpy()
+        S = S.reshape(batch_shape + S.shape[-3:])
+        if self.out_type == "list":
+            return self._to_list(S, batch_shape)
+        return S
+
+    def pooled(self, input):
+        """Per-coefficient spatial [mean | std] (population std): (..., 2K) float32."""
+        if not isinstance(input, np.ndarray):
+            raise TypeError("The input should be a NumPy array.")
+        self._check_spatial(input.shape, "array")
+        require_gpu()
+        import torch
+        batch_shape = input.shape[:-2]
+        x = np.ascontiguousarray(input, dtype=np.float32).reshape((-1,) + input.shape[-2:])
+        xd = torch.from_numpy(x).to("cuda")
+        F = scatter_device(xd, self.M, self.N, self.J, self.L, self.max_order, self.pre_pad,
+                           pooled=True)
+        return F.cpu().numpy().reshape(batch_shape + (2 * self.K,))
+
+    __call__ = scattering
