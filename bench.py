@@ -1,0 +1,275 @@
+#!/usr/bin/env python3
+"""Headline benchmark: BASELINE.json metric "patches/sec (whole node) + HBM-roofline %,
+64x64 RGB WST J=4 L=8 order-2" on BASELINE config 2 (batch of 1024 64x64 RGB patches per GPU).
+
+A "step" = one Scattering2D(J=4, L=8, order 2) pass over one resident batch of 1024 RGB patches
+(3072 planes) -> full coefficient tensor (1024, 3, 417, 4, 4) fp32, via the C ABI (libwst_hip.so).
+Inputs are synthetic uint8/255 patches (mimicking load_rgb_image, train_and_save_model.py:51-56)
+generated once and resident in HBM before timing.
+
+Multi-GPU (torchrun, one process per GPU): the patches shard across ranks with no data-path
+collective (weak scaling: every rank processes its own 1024-patch batch); value = all patches of
+all ranks / max-over-ranks wall time.  `--gather` additionally times an RCCL all-gather of the
+pooled features (reported separately, never in `value`).
+
+Extra JSON fields:
+  roofline     : dominant kernel (k_order12) algorithmic FLOP per launch / HIP-event launch time
+                 vs the fp32 peak (SURVEY §8(d) flop convention 5 n^2 log2 n^2 per n x n FFT);
+                 traffic from committed rocprofv3 PMC passes when they match this library build.
+  cpu_baseline : the float64 oracle (oracle/kymatio_ref.py, a port of kymatio 0.3.0) run the way
+                 the reference runs it (plan rebuilt per patch, 3 serial channel calls + mean/std,
+                 train_and_save_model.py:346-378), single core, bounded sample, rank 0 at N=1.
+"""
+import argparse
+import hashlib
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "patches/sec (whole node) + HBM-roofline %, 64x64 RGB WST J=4 L=8 order-2"
+FP32_PEAK_TFLOPS = 157.3      # MI355X FP32 vector == f32 MFMA dense peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    "c2": dict(workload="c2: 1024 x 64x64 RGB patches, Scattering2D J=4 L=8 order-2 (per GPU)",
+               C=3, M=64, N=64, J=4, L=8, batch=1024),
+    "c1": dict(workload="c1: 64x64 RGB patch, J=2 L=8 order-2 (batch as given)",
+               C=3, M=64, N=64, J=2, L=8, batch=1024),
+}
+
+
+def fft_flops(n1, n2):
+    n = n1 * n2
+    return 5.0 * n * math.log2(n) if n > 1 else 0.0
+
+
+def alg_flops_per_plane(PM, PN, J, L, max_order=2):
+    """kymatio cascade FFT FLOPs split by the kernel that performs each path."""
+    mM, mN = PM >> J, PN >> J
+    prep = fft_flops(PM, PN) + fft_flops(mM, mN)                    # X^ and S0
+    per_j1 = []
+    for j1 in range(J):
+        n1 = (PM >> j1, PN >> j1)
+        f = L * (2 * fft_flops(*n1) + fft_flops(mM, mN))            # U1 ifft/fft + S1
+        if max_order >= 2:
+            for j2 in range(j1 + 1, J):
+                n2 = (PM >> j2, PN >> j2)
+                f += L * L * (2 * fft_flops(*n2) + fft_flops(mM, mN))   # U2 ifft/fft + S2
+        per_j1.append(f)
+    return prep, per_j1
+
+
+def lib_sha():
+    from wst_amd import _lib
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_traffic(sha):
+    """HBM bytes per k_order12 launch from committed rocprofv3 PMC passes of this exact build."""
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for name in sorted(os.listdir(pdir), reverse=True):
+        if name.startswith("pmc_") and name.endswith(".json"):
+            try:
+                d = json.load(open(os.path.join(pdir, name)))
+            except Exception:
+                continue
+            if d.get("lib_sha") == sha and "k_order12_hbm_bytes_per_launch" in d:
+                return d["k_order12_hbm_bytes_per_launch"]
+    return None
+
+
+def cpu_baseline(cfg, budget_s):
+    """Reference-faithful CPU path on the float64 oracle: per patch, Scattering2D rebuilt
+    (train_and_save_model.py:359) and 3 serial channel calls + mean/std (:364-376)."""
+    import numpy as np
+    try:
+        from threadpoolctl import threadpool_limits
+        lim = threadpool_limits(1)
+    except Exception:
+        lim = None
+    from oracle import kymatio_ref as kr
+    rng = np.random.default_rng(1)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        img = rng.integers(0, 256, (cfg["C"], cfg["M"], cfg["N"]), dtype=np.uint8).astype(np.float32) / 255
+        kr.extract_wst_features(img, J=cfg["J"], L=cfg["L"])      # builds its own Scattering2D
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or n >= 256:
+            break
+    faithful = n / el
+    # cached plan, one batched call (best case for the same float64 code on one core)
+    sc = kr.Scattering2D(J=cfg["J"], shape=(cfg["M"], cfg["N"]), L=cfg["L"])
+    xb = rng.integers(0, 256, (16, cfg["C"], cfg["M"], cfg["N"]), dtype=np.uint8).astype(np.float32) / 255
+    t1 = time.perf_counter()
+    S = sc(xb)
+    np.mean(S, axis=(-2, -1)), np.std(S, axis=(-2, -1))
+    cached = 16 / (time.perf_counter() - t1)
+    if lim is not None:
+        lim.unregister() if hasattr(lim, "unregister") else None
+    return {
+        "value": round(faithful, 3), "unit": "patches/s", "cores": 1, "kind": "port",
+        "sample": (f"{n} patches of ({cfg['C']},{cfg['M']},{cfg['N']}) in {el:.1f} s: oracle/kymatio_ref.py "
+                   f"float64 port of kymatio 0.3.0, plan rebuilt per patch + 3 channel calls + mean/std "
+                   f"(train_and_save_model.py:346-378), single thread"),
+        "cached_plan_batched_value": round(cached, 3),
+        "host_cpu_count": os.cpu_count(),
+        "host_affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="patches per GPU (default: config)")
+    ap.add_argument("--pooled", action="store_true", help="fused mean/std epilogue output")
+    ap.add_argument("--gather", action="store_true", help="also time an RCCL all-gather of features")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-iters", type=int, default=3)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import wst_amd  # noqa: F401
+    from wst_amd import _lib
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = dict(CONFIGS[args.config])
+    B = args.batch or cfg["batch"]
+    C, M, N, J, L = cfg["C"], cfg["M"], cfg["N"], cfg["J"], cfg["L"]
+    planes = B * C
+
+    rng = np.random.default_rng(1 + rank)
+    x = torch.from_numpy(rng.integers(0, 256, (B, C, M, N), dtype=np.uint8).astype(np.float32) / 255).to(dev)
+    plan = _lib.Plan(M, N, J, L, 2, False)
+    K, Mo, No = plan.K, plan.Mo, plan.No
+    out = torch.empty((planes, 2 * K) if args.pooled else (planes, K, Mo, No), dtype=torch.float32, device=dev)
+    ws_bytes = plan.workspace_bytes(min(planes, 2048))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        plan.forward(x.data_ptr(), planes, out.data_ptr(), args.pooled, ws.data_ptr(), ws_bytes, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    ms_per_step = dt / args.steps * 1e3
+    value = B * world * args.steps / dt
+
+    # per-kernel HIP-event durations on the launch stream (separate, untimed passes)
+    nslots = 1 + J
+    acc = [0.0] * nslots
+    for _ in range(args.profile_iters):
+        ms = plan.forward_profiled(x.data_ptr(), planes, out.data_ptr(), args.pooled, ws.data_ptr(),
+                                   ws_bytes, stream, nslots)
+        acc = [a + b for a, b in zip(acc, ms)]
+    kms = [a / args.profile_iters for a in acc]
+    nchunks = math.ceil(planes / min(planes, 2048))
+    prep_f, per_j1 = alg_flops_per_plane(plan.PM, plan.PN, J, L)
+    k12_ms = sum(kms[1:])
+    k12_launches = J * nchunks
+    k12_flop = planes * sum(per_j1)
+    achieved = k12_flop / (k12_ms * 1e-3) / 1e12
+    sha = lib_sha()
+    traffic = pmc_traffic(sha)
+    roofline = {
+        "bound": "mfma", "pipe": "fp32 (VALU FFT butterflies; gfx950 f32 MFMA shares the 157.3 TFLOP/s peak)",
+        "kernel": "k_order12", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
+        "traffic": traffic,
+        "launches_per_step": k12_launches,
+        "avg_launch_ms": round(k12_ms / k12_launches, 4),
+        "alg_flop_per_launch": round(k12_flop / k12_launches),
+        "kernel_ms_per_step": {"k_prep": round(kms[0], 4),
+                               **{f"k_order12_j1={j}": round(kms[1 + j], 4) for j in range(J)}},
+        "lib_sha": sha,
+    }
+    patch_flop = C * (prep_f + sum(per_j1))
+    patch_bytes = C * M * N * 4 + (C * 2 * K * 4 if args.pooled else C * K * Mo * No * 4)
+    rate_per_gpu = value / world
+    step_roof = {
+        "alg_flop_per_patch": round(patch_flop), "alg_bytes_per_patch": patch_bytes,
+        "valu_frac": round(patch_flop * rate_per_gpu / (FP32_PEAK_TFLOPS * 1e12), 5),
+        "hbm_roofline_pct": round(100 * patch_bytes * rate_per_gpu / (HBM_PEAK_GBS * 1e9), 5),
+    }
+
+    gather = None
+    if args.gather and world > 1:
+        feats = torch.empty((planes, 2 * K), dtype=torch.float32, device=dev)
+        plan.forward(x.data_ptr(), planes, feats.data_ptr(), True, ws.data_ptr(), ws_bytes, stream)
+        allf = torch.empty((world * planes, 2 * K), dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(allf, feats)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        g0 = time.perf_counter()
+        for _ in range(5):
+            dist.all_gather_into_tensor(allf, feats)
+        torch.cuda.synchronize(dev)
+        gather = {"what": "pooled features all_gather", "bytes_per_rank": feats.numel() * 4,
+                  "ms": round((time.perf_counter() - g0) / 5 * 1e3, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, args.cpu_budget)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "patches/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic uint8/255 RGB patches (load_rgb_image distribution), resident in HBM",
+            "config": {"workload": cfg["workload"], "patches_per_gpu": B, "channels": C,
+                       "shape": [M, N], "J": J, "L": L, "max_order": 2, "K": K,
+                       "output": "pooled [mean|std]" if args.pooled else f"full ({K},{Mo},{No}) fp32",
+                       "parallelism": f"patch-sharded x{world} (no collective in step)"},
+            "roofline": roofline, "step_roofline": step_roof, "cpu_baseline": cpu,
+        }
+        if gather:
+            line["gather"] = gather
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -87,6 +87,17 @@ int wst_forward(const wst_plan* plan, const float* d_in, int64_t nbatch, float* 
                 void* d_workspace, size_t workspace_bytes, void* stream);
 
 /*
+ * wst_forward + per-kernel timing with HIP events recorded on `stream` around every launch
+ * (synchronises the stream before returning).  kernel_ms[0] = sum of k_prep launches,
+ * kernel_ms[1 + j1] = sum of the k_order12 launches at scale j1 (0 <= j1 < J); n_kernel_ms is
+ * the capacity of kernel_ms (entries beyond 1 + J are left untouched).  Used by bench.py for the
+ * roofline's per-kernel durations; not meant for production calls.
+ */
+int wst_forward_profiled(const wst_plan* plan, const float* d_in, int64_t nbatch, float* d_out,
+                         int pooled, void* d_workspace, size_t workspace_bytes, void* stream,
+                         float* kernel_ms, int n_kernel_ms);
+
+/*
  * Host-only filter inspection (no GPU needed; used by the CPU test-suite to pin the library's
  * float64 filter construction against the oracle).  kind:
  *   0 = psi_{j,l} Fourier level r        -> (PM>>r) x (PN>>r) doubles

@@ -22,7 +22,7 @@ ABI_VERSION = 1
 EXPORTS = (
     "wst_abi_version", "wst_last_error", "wst_plan_create", "wst_plan_destroy",
     "wst_output_shape", "wst_padded_shape", "wst_workspace_bytes", "wst_forward",
-    "wst_host_filter",
+    "wst_forward_profiled", "wst_host_filter",
 )
 
 _lib = None
@@ -68,6 +68,9 @@ def load() -> ctypes.CDLL:
         lib.wst_workspace_bytes.argtypes = [c_vp, c_i64, ctypes.POINTER(c_sz)]
         lib.wst_forward.restype = c_int
         lib.wst_forward.argtypes = [c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_sz, c_vp]
+        lib.wst_forward_profiled.restype = c_int
+        lib.wst_forward_profiled.argtypes = [c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_sz, c_vp,
+                                             ctypes.POINTER(ctypes.c_float), c_int]
         lib.wst_host_filter.restype = c_int
         lib.wst_host_filter.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                         ctypes.POINTER(ctypes.c_double), c_i64]
@@ -126,6 +129,16 @@ class Plan:
                                  ctypes.c_void_p(d_out), 1 if pooled else 0,
                                  ctypes.c_void_p(d_ws or None), int(ws_bytes),
                                  ctypes.c_void_p(stream or None)))
+
+    def forward_profiled(self, d_in: int, nbatch: int, d_out: int, pooled: bool, d_ws: int,
+                         ws_bytes: int, stream: int, nslots: int):
+        """wst_forward_profiled: returns per-kernel summed milliseconds (list of nslots)."""
+        ms = (ctypes.c_float * nslots)()
+        check(load().wst_forward_profiled(self._h, ctypes.c_void_p(d_in), int(nbatch),
+                                          ctypes.c_void_p(d_out), 1 if pooled else 0,
+                                          ctypes.c_void_p(d_ws or None), int(ws_bytes),
+                                          ctypes.c_void_p(stream or None), ms, nslots))
+        return list(ms)
 
     def close(self):
         if getattr(self, "_h", None) is not None and _lib is not None:

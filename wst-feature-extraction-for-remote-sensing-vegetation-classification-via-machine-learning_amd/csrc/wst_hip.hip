@@ -606,8 +606,46 @@ int wst_workspace_bytes(const wst_plan* plan, int64_t nbatch, size_t* bytes) {
     return WST_OK;
 }
 
-int wst_forward(const wst_plan* plan, const float* d_in, int64_t nbatch, float* d_out, int pooled,
-                void* d_workspace, size_t workspace_bytes, void* stream_) {
+}  // extern "C"
+
+namespace {
+
+// Launch-time timer: when `kms` is non-null, every launch is bracketed by events on `stream`
+// and its duration is added to kms[slot].
+struct LaunchTimer {
+    float* kms = nullptr;
+    int nkms = 0;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    ~LaunchTimer() {
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+    }
+    int init(float* k, int n) {
+        kms = k;
+        nkms = n;
+        if (!kms) return WST_OK;
+        for (int i = 0; i < n; ++i) kms[i] = 0.f;
+        WST_HIP_CHECK(hipEventCreate(&e0));
+        WST_HIP_CHECK(hipEventCreate(&e1));
+        return WST_OK;
+    }
+    int begin(hipStream_t s) {
+        if (kms) WST_HIP_CHECK(hipEventRecord(e0, s));
+        return WST_OK;
+    }
+    int end(hipStream_t s, int slot) {
+        if (!kms) return WST_OK;
+        WST_HIP_CHECK(hipEventRecord(e1, s));
+        WST_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        WST_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (slot < nkms) kms[slot] += ms;
+        return WST_OK;
+    }
+};
+
+int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float* d_out, int pooled,
+                 void* d_workspace, size_t workspace_bytes, void* stream_, float* kms, int nkms) {
     if (!plan) return fail(WST_ERR_INVALID, "plan is NULL");
     if (nbatch < 0) return fail(WST_ERR_INVALID, "nbatch < 0");
     if (nbatch == 0) return WST_OK;
@@ -643,20 +681,45 @@ int wst_forward(const wst_plan* plan, const float* d_in, int64_t nbatch, float* 
     if (chunk < 1) return fail(WST_ERR_INVALID, "workspace smaller than one padded plane");
     const int inM = plan->dp.pre_pad ? g.PM : g.M, inN = plan->dp.pre_pad ? g.PN : g.N;
     float2* xhat = reinterpret_cast<float2*>(ws);
+    LaunchTimer timer;
+    int rc;
+    if ((rc = timer.init(kms, nkms)) != WST_OK) return rc;
     for (int64_t c0 = 0; c0 < nbatch; c0 += chunk) {
         const int nimg = static_cast<int>(std::min<int64_t>(chunk, nbatch - c0));
+        if ((rc = timer.begin(stream)) != WST_OK) return rc;
         hipLaunchKernelGGL(k_prep, dim3(nimg), dim3(plan->prep_threads), plan->prep_lds, stream,
                            plan->dp, d_in + c0 * inM * inN, static_cast<long long>(c0), xhat, d_out,
                            pooled);
         WST_HIP_CHECK(hipGetLastError());
+        if ((rc = timer.end(stream, 0)) != WST_OK) return rc;
         for (int j1 = 0; j1 < g.J; ++j1) {
+            if ((rc = timer.begin(stream)) != WST_OK) return rc;
             hipLaunchKernelGGL(k_order12, dim3(nimg * g.L), dim3(plan->k1_threads[j1]),
                                plan->k1_lds[j1], stream, plan->dp, j1, plan->k1_G[j1], nimg,
                                static_cast<long long>(c0), xhat, d_out, pooled);
             WST_HIP_CHECK(hipGetLastError());
+            if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
         }
     }
     return WST_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wst_forward(const wst_plan* plan, const float* d_in, int64_t nbatch, float* d_out, int pooled,
+                void* d_workspace, size_t workspace_bytes, void* stream) {
+    return forward_impl(plan, d_in, nbatch, d_out, pooled, d_workspace, workspace_bytes, stream,
+                        nullptr, 0);
+}
+
+int wst_forward_profiled(const wst_plan* plan, const float* d_in, int64_t nbatch, float* d_out,
+                         int pooled, void* d_workspace, size_t workspace_bytes, void* stream,
+                         float* kernel_ms, int n_kernel_ms) {
+    if (!kernel_ms || n_kernel_ms < 1) return fail(WST_ERR_INVALID, "kernel_ms is NULL/empty");
+    return forward_impl(plan, d_in, nbatch, d_out, pooled, d_workspace, workspace_bytes, stream,
+                        kernel_ms, n_kernel_ms);
 }
 
 int wst_host_filter(int M, int N, int J, int L, int kind, int j, int l, int r, double* out,
@@ -667,7 +730,11 @@ int wst_host_filter(int M, int N, int J, int L, int kind, int j, int l, int r, d
     std::string err;
     if (!wst::make_geometry(M, N, J, L, 2, g, err)) return fail(WST_ERR_INVALID, err);
     try {
-        wst::FilterBank fb = wst::build_filter_bank(g);
+        // cache the last bank: the test-suite inspects every filter of one geometry in turn
+        static thread_local std::unique_ptr<wst::FilterBank> cached;
+        if (!cached || cached->g.M != M || cached->g.N != N || cached->g.J != J || cached->g.L != L)
+            cached.reset(new wst::FilterBank(wst::build_filter_bank(g)));
+        const wst::FilterBank& fb = *cached;
         std::vector<double> v;
         if (kind == 0) {
             if (j < 0 || j >= J || l < 0 || l >= L) return fail(WST_ERR_INVALID, "bad (j, l)");
