@@ -109,6 +109,16 @@ int wst_forward_profiled(const wst_plan* plan, const float* d_in, int64_t nbatch
 int wst_host_filter(int M, int N, int J, int L, int kind, int j, int l, int r, double* out,
                     int64_t len);
 
+/*
+ * Host emulation of the device line-FFT engine (test hook, no GPU): runs the exact per-unit code
+ * of the LDS FFTs (csrc/fft_lds.h) sequentially on `data` (complex64 interleaved), in place.
+ * Line (b, l) element e lives at complex index b*bs + l*ls + e*es; n is the line length,
+ * `threads` the workgroup size whose round structure is emulated; inverse is unnormalised.
+ * Sizes without a compiled FFT run the generic DFT the kernels fall back to.
+ */
+int wst_host_fft_lines(int n, int inverse, float* data, int nb, int bs, int nl, int ls, int es,
+                       int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -22,7 +22,7 @@ ABI_VERSION = 1
 EXPORTS = (
     "wst_abi_version", "wst_last_error", "wst_plan_create", "wst_plan_destroy",
     "wst_output_shape", "wst_padded_shape", "wst_workspace_bytes", "wst_forward",
-    "wst_forward_profiled", "wst_host_filter",
+    "wst_forward_profiled", "wst_host_filter", "wst_host_fft_lines",
 )
 
 _lib = None
@@ -74,6 +74,8 @@ def load() -> ctypes.CDLL:
         lib.wst_host_filter.restype = c_int
         lib.wst_host_filter.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                         ctypes.POINTER(ctypes.c_double), c_i64]
+        lib.wst_host_fft_lines.restype = c_int
+        lib.wst_host_fft_lines.argtypes = [c_int, c_int, c_vp] + [c_int] * 6
         v = lib.wst_abi_version()
         if v != ABI_VERSION:
             raise RuntimeError(f"{LIB_NAME} ABI version {v} != expected {ABI_VERSION}; rebuild it")
@@ -96,6 +98,13 @@ def host_filter(M, N, J, L, kind, j, l, r, size) -> np.ndarray:
     check(load().wst_host_filter(M, N, J, L, kind, j, l, r,
                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), size))
     return out
+
+
+def host_fft_lines(data: np.ndarray, n, inverse, nb, bs, nl, ls, es, threads=256) -> None:
+    """In-place host emulation of the device line FFT on a complex64 buffer (test hook)."""
+    assert data.dtype == np.complex64 and data.flags.c_contiguous
+    check(load().wst_host_fft_lines(int(n), 1 if inverse else 0, data.ctypes.data, int(nb),
+                                    int(bs), int(nl), int(ls), int(es), int(threads)))
 
 
 class Plan:

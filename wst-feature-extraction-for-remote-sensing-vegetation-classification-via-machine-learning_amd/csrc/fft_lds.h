@@ -1,0 +1,363 @@
+// LDS-resident batched 1-D / 2-D FFTs for gfx950 (wave64).
+//
+// * rfft<R, INV>(x): length-R DFT of a register array, fully unrolled at compile time.  Composite
+//   R: decimation-in-time Cooley-Tukey R = P*Q with compile-time twiddles (constexpr double sin/cos
+//   rounded once to fp32); R in {2, 4}: hand butterflies; odd primes: symmetric direct DFT.
+// * LineFFT<N, INV>: N-point transforms along lines of LDS arrays.  N <= 16 (or prime): one unit
+//   per line, in place.  Otherwise the four-step split N = N1*N2:
+//     stage A  unit (line, n2): DFT-N1 over elements n2 + N2*n1, times W_N^(n2*k1), in place;
+//     stage B  unit (line, k1): DFT-N2 over the contiguous block N2*k1 + n2 -> stored to the
+//              natural position k1 + N1*k2 (all loads of a round of lines precede its stores).
+//   Lanes walk consecutive LINES: along rows the row stride is odd (conflict-free b64 access on
+//   32-lane halves), along columns consecutive lines are contiguous.
+//   Natural order in, natural order out; INV = unnormalised inverse.
+// The per-unit bodies are __host__ __device__ so the CPU test-suite can run the exact index math
+// through a sequential emulation (fft_lines_host) against numpy.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+#include <utility>
+
+#define WST_HD __host__ __device__ __forceinline__
+
+// Every level size of a plan is odd * 2^k (P = (M/2^J + 2) * 2^J), so kernels are instantiated
+// per "size family" (the odd part of P) and compile only that family's FFTs (kMaxFamilyN bounds
+// the LDS-resident sizes).  Families with compiled FFTs: 1, 3, 5, 9, 17 (others: generic DFT).
+#define WST_FFT_SIZES(X) \
+    X(2) X(3) X(4) X(5) X(6) X(8) X(9) X(10) X(12) X(16) X(17) X(18) X(20) X(24) X(32) X(34) \
+    X(36) X(40) X(48) X(64) X(68) X(72) X(80) X(96) X(128) X(136)
+
+namespace wstfft {
+
+constexpr int kMaxFamilyN = 136;
+
+// ---------------------------------------------------------------------------------------------
+// compile-time trigonometry (double), exact quarter-turn reduction from integers
+// ---------------------------------------------------------------------------------------------
+constexpr double kHalfPi = 1.5707963267948966192313216916397514;
+
+constexpr double taylor_sin(double x) {
+    double x2 = x * x, term = x, sum = x;
+    for (int i = 1; i < 14; ++i) {
+        term *= -x2 / ((2.0 * i) * (2.0 * i + 1.0));
+        sum += term;
+    }
+    return sum;
+}
+constexpr double taylor_cos(double x) {
+    double x2 = x * x, term = 1.0, sum = 1.0;
+    for (int i = 1; i < 14; ++i) {
+        term *= -x2 / ((2.0 * i - 1.0) * (2.0 * i));
+        sum += term;
+    }
+    return sum;
+}
+// cos / sin of 2 pi m / n
+constexpr double cos2pi(long long m, long long n) {
+    const long long mm = ((m % n) + n) % n;
+    const long long q = (4 * mm + n / 2) / n;  // nearest quarter turn
+    const double d = kHalfPi * static_cast<double>(4 * mm - q * n) / static_cast<double>(n);
+    switch (q & 3) {
+        case 0: return taylor_cos(d);
+        case 1: return -taylor_sin(d);
+        case 2: return -taylor_cos(d);
+        default: return taylor_sin(d);
+    }
+}
+constexpr double sin2pi(long long m, long long n) {
+    const long long mm = ((m % n) + n) % n;
+    const long long q = (4 * mm + n / 2) / n;
+    const double d = kHalfPi * static_cast<double>(4 * mm - q * n) / static_cast<double>(n);
+    switch (q & 3) {
+        case 0: return taylor_sin(d);
+        case 1: return taylor_cos(d);
+        case 2: return -taylor_sin(d);
+        default: return -taylor_cos(d);
+    }
+}
+
+template <int B, int E, typename F>
+WST_HD void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+constexpr bool is_prime(int n) {
+    if (n < 2) return false;
+    for (int p = 2; p * p <= n; ++p)
+        if (n % p == 0) return false;
+    return true;
+}
+constexpr int pick_radix(int n) {  // outer radix of the register Cooley-Tukey split
+    if (n % 4 == 0 && n != 4) return 4;
+    for (int p = 2; p <= n; ++p)
+        if (n % p == 0) return p;
+    return n;
+}
+
+WST_HD float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+WST_HD float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+
+// x * W_R^M (forward W = exp(-2 pi i / R); INV conjugates), trivial twiddles short-cut.
+template <int R, int M, bool INV>
+WST_HD float2 twiddle(float2 x) {
+    constexpr int m = ((M % R) + R) % R;
+    if constexpr (m == 0) {
+        return x;
+    } else if constexpr (2 * m == R) {
+        return make_float2(-x.x, -x.y);
+    } else if constexpr (4 * m == R) {  // forward: -i, inverse: +i
+        return INV ? make_float2(-x.y, x.x) : make_float2(x.y, -x.x);
+    } else if constexpr (4 * m == 3 * R) {  // forward: +i, inverse: -i
+        return INV ? make_float2(x.y, -x.x) : make_float2(-x.y, x.x);
+    } else {
+        constexpr float c = static_cast<float>(cos2pi(m, R));
+        constexpr float s = static_cast<float>(INV ? sin2pi(m, R) : -sin2pi(m, R));
+        return make_float2(fmaf(x.x, c, -x.y * s), fmaf(x.x, s, x.y * c));
+    }
+}
+
+template <int R, bool INV>
+WST_HD void rfft(float2 (&x)[R]) {
+    if constexpr (R == 1) {
+        return;
+    } else if constexpr (R == 2) {
+        const float2 t = x[0];
+        x[0] = cadd(t, x[1]);
+        x[1] = csub(t, x[1]);
+    } else if constexpr (R == 4) {
+        const float2 a0 = cadd(x[0], x[2]), a1 = csub(x[0], x[2]);
+        const float2 b0 = cadd(x[1], x[3]), b1 = csub(x[1], x[3]);
+        const float2 rb1 = INV ? make_float2(-b1.y, b1.x) : make_float2(b1.y, -b1.x);
+        x[0] = cadd(a0, b0);
+        x[2] = csub(a0, b0);
+        x[1] = cadd(a1, rb1);
+        x[3] = csub(a1, rb1);
+    } else if constexpr (is_prime(R)) {
+        // symmetric direct DFT: a_n = x_n + x_{R-n}, b_n = x_n - x_{R-n}
+        constexpr int H = (R - 1) / 2;
+        float2 a[H + 1], b[H + 1];
+        const float2 x0 = x[0];
+        float2 sum = x0;
+        static_for<1, H + 1>([&](auto nc) {
+            constexpr int n = decltype(nc)::value;
+            a[n] = cadd(x[n], x[R - n]);
+            b[n] = csub(x[n], x[R - n]);
+            sum = cadd(sum, a[n]);
+        });
+        static_for<1, H + 1>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            float tr = x0.x, ti = x0.y, ur = 0.f, ui = 0.f;
+            static_for<1, H + 1>([&](auto nc) {
+                constexpr int n = decltype(nc)::value;
+                constexpr float c = static_cast<float>(cos2pi(static_cast<long long>(n) * k, R));
+                constexpr float s = static_cast<float>(sin2pi(static_cast<long long>(n) * k, R));
+                tr = fmaf(a[n].x, c, tr);
+                ti = fmaf(a[n].y, c, ti);
+                ur = fmaf(b[n].x, s, ur);
+                ui = fmaf(b[n].y, s, ui);
+            });
+            // forward: X[k] = t - i u, X[R-k] = t + i u ; inverse swaps the signs
+            if constexpr (!INV) {
+                x[k] = make_float2(tr + ui, ti - ur);
+                x[R - k] = make_float2(tr - ui, ti + ur);
+            } else {
+                x[k] = make_float2(tr - ui, ti + ur);
+                x[R - k] = make_float2(tr + ui, ti - ur);
+            }
+        });
+        x[0] = sum;
+    } else {
+        constexpr int P = pick_radix(R);
+        constexpr int Q = R / P;
+        float2 y[P][Q];
+        static_for<0, P>([&](auto pc) {
+            constexpr int p = decltype(pc)::value;
+            static_for<0, Q>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                y[p][q] = x[p + P * q];
+            });
+            rfft<Q, INV>(y[p]);
+        });
+        static_for<0, Q>([&](auto k1c) {
+            constexpr int k1 = decltype(k1c)::value;
+            float2 z[P];
+            static_for<0, P>([&](auto pc) {
+                constexpr int p = decltype(pc)::value;
+                z[p] = twiddle<R, p * k1, INV>(y[p][k1]);
+            });
+            rfft<P, INV>(z);
+            static_for<0, P>([&](auto k2c) {
+                constexpr int k2 = decltype(k2c)::value;
+                x[k1 + Q * k2] = z[k2];
+            });
+        });
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// four-step line transforms
+// ---------------------------------------------------------------------------------------------
+constexpr int split_n2(int n) {  // N2 = largest divisor <= sqrt(n); 1 means a single stage
+    if (n <= 16 || is_prime(n)) return 1;
+    int best = 1;
+    for (int d = 2; d * d <= n; ++d)
+        if (n % d == 0) best = d;
+    return best;
+}
+
+WST_HD float2 cmul_tw(float2 a, float2 w, bool conj) {
+    const float wy = conj ? -w.y : w.y;
+    return make_float2(fmaf(a.x, w.x, -a.y * wy), fmaf(a.x, wy, a.y * w.x));
+}
+
+// Geometry of a batch of lines: line (b, l) element e at base[b*bs + l*ls + e*es].
+struct Lines {
+    int nb, bs, nl, ls, es;
+    WST_HD int nlines() const { return nb * nl; }
+    WST_HD int offset(int line) const {
+        const int b = line / nl;
+        return b * bs + (line - b * nl) * ls;
+    }
+};
+
+template <int N, bool INV>
+struct LineFFT {
+    static constexpr int N2 = split_n2(N);
+    static constexpr int N1 = N / N2;
+    static constexpr int UPT = (N2 <= 4) ? 4 : (N2 <= 8 ? 2 : 1);  // stage-B units per thread
+
+    // single stage: unit = whole line
+    static WST_HD void single_unit(float2* base, const Lines& g, int u) {
+        float2* p = base + g.offset(u);
+        float2 v[N];
+        static_for<0, N>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            v[e] = p[e * g.es];
+        });
+        rfft<N, INV>(v);
+        static_for<0, N>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            p[e * g.es] = v[e];
+        });
+    }
+    // stage A: unit u -> (line = u % nlines, n2 = u / nlines)
+    static WST_HD void stageA_unit(float2* base, const Lines& g, const float2* tw, int u) {
+        const int nlines = g.nlines();
+        const int line = u % nlines;
+        const int n2 = u / nlines;
+        float2* p = base + g.offset(line) + n2 * g.es;
+        float2 v[N1];
+        static_for<0, N1>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            v[e] = p[e * N2 * g.es];
+        });
+        rfft<N1, INV>(v);
+        static_for<1, N1>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            v[k] = cmul_tw(v[k], tw[n2 * k], INV);
+        });
+        static_for<0, N1>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            p[e * N2 * g.es] = v[e];
+        });
+    }
+    // stage B load+compute: round lines [L0, L0+nlr), unit w -> (line = L0 + w % nlr, k1 = w / nlr)
+    static WST_HD int stageB_load(const float2* base, const Lines& g, int L0, int nlr, int w,
+                                  float2 (&v)[N2]) {
+        const int line = L0 + w % nlr;
+        const int k1 = w / nlr;
+        const int lb = g.offset(line);
+        const float2* p = base + lb + (N2 * k1) * g.es;
+        static_for<0, N2>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            v[e] = p[e * g.es];
+        });
+        rfft<N2, INV>(v);
+        return lb + k1 * g.es;
+    }
+    static WST_HD void stageB_store(float2* base, const Lines& g, int addr, const float2 (&v)[N2]) {
+        float2* q = base + addr;
+        static_for<0, N2>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            q[e * N1 * g.es] = v[e];
+        });
+    }
+    static WST_HD int lines_per_round(int T) {
+        const int l = (T * UPT) / N1;
+        return l < 1 ? 1 : l;
+    }
+};
+
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+// Device driver.  Ends with a barrier.
+template <int N, bool INV>
+__device__ void fft_lines(float2* base, const Lines g, const float2* tw) {
+    using F = LineFFT<N, INV>;
+    const int T = blockDim.x;
+    const int nlines = g.nlines();
+    if constexpr (F::N2 == 1) {
+        for (int u = threadIdx.x; u < nlines; u += T) F::single_unit(base, g, u);
+        __syncthreads();
+    } else {
+        const int unitsA = nlines * F::N2;
+        for (int u = threadIdx.x; u < unitsA; u += T) F::stageA_unit(base, g, tw, u);
+        __syncthreads();
+        const int lpr = F::lines_per_round(T);
+        for (int L0 = 0; L0 < nlines; L0 += lpr) {
+            const int nlr = min(lpr, nlines - L0);
+            const int units = nlr * F::N1;
+            float2 v[F::UPT][F::N2];
+            int addr[F::UPT];
+            static_for<0, F::UPT>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                const int w = threadIdx.x + i * T;
+                addr[i] = (w < units) ? F::stageB_load(base, g, L0, nlr, w, v[i]) : -1;
+            });
+            __syncthreads();
+            static_for<0, F::UPT>([&](auto ic) {
+                constexpr int i = decltype(ic)::value;
+                if (addr[i] >= 0) F::stageB_store(base, g, addr[i], v[i]);
+            });
+        }
+        __syncthreads();
+    }
+}
+#endif
+
+// Host emulation with the same unit bodies (sequential "threads", barriers implicit).
+template <int N, bool INV>
+inline void fft_lines_host(float2* base, const Lines g, const float2* tw, int T) {
+    using F = LineFFT<N, INV>;
+    const int nlines = g.nlines();
+    if constexpr (F::N2 == 1) {
+        for (int u = 0; u < nlines; ++u) F::single_unit(base, g, u);
+    } else {
+        for (int u = 0; u < nlines * F::N2; ++u) F::stageA_unit(base, g, tw, u);
+        const int lpr = F::lines_per_round(T);
+        for (int L0 = 0; L0 < nlines; L0 += lpr) {
+            const int nlr = (lpr < nlines - L0) ? lpr : nlines - L0;
+            const int units = nlr * F::N1;
+            float2* v = new float2[static_cast<size_t>(units) * F::N2];
+            int* addr = new int[units];
+            for (int w = 0; w < units; ++w) {
+                float2 tmp[F::N2];
+                addr[w] = F::stageB_load(base, g, L0, nlr, w, tmp);
+                for (int e = 0; e < F::N2; ++e) v[static_cast<size_t>(w) * F::N2 + e] = tmp[e];
+            }
+            for (int w = 0; w < units; ++w) {
+                float2 tmp[F::N2];
+                for (int e = 0; e < F::N2; ++e) tmp[e] = v[static_cast<size_t>(w) * F::N2 + e];
+                F::stageB_store(base, g, addr[w], tmp);
+            }
+            delete[] v;
+            delete[] addr;
+        }
+    }
+}
+
+}  // namespace wstfft

@@ -32,6 +32,7 @@
 #include <string>
 #include <vector>
 
+#include "fft_lds.h"
 #include "filter_bank.h"
 #include "wst_hip.h"
 
@@ -92,13 +93,12 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
     return s;
 }
 
-// Batched in-place DFT along one axis.  Array b, line l, element e lives at
-// base[b*bs + l*ls + e*es].  Lines are processed in chunks of whole lines that fit the register
-// tile (T * kMaxO outputs): read phase -> barrier -> write phase.  Ends with a barrier.
-__device__ void lds_dft_lines(float2* base, int nb, int bs, int nl, int ls, int es, int n,
-                              const float2* tw, bool inverse) {
+// Generic O(n) DFT along lines (fallback for sizes without a compiled FFT).  Lines are processed
+// in chunks of whole lines that fit the register tile: read phase -> barrier -> write phase.
+__device__ void lds_dft_lines_generic(float2* base, const wstfft::Lines g, int n, const float2* tw,
+                                      bool inverse) {
     const int T = blockDim.x;
-    const int lines_total = nb * nl;
+    const int lines_total = g.nlines();
     int lpc = (T * kMaxO) / n;
     if (lpc < 1) lpc = 1;
     const float sgn = inverse ? -1.f : 1.f;
@@ -115,14 +115,12 @@ __device__ void lds_dft_lines(float2* base, int nb, int bs, int nl, int ls, int 
             if (o < nout) {
                 const int lc = o / n;
                 const int k = o - lc * n;
-                const int Lg = l0 + lc;
-                const int b = Lg / nl;
-                const int l = Lg - b * nl;
-                const float2* src = base + b * bs + l * ls;
+                const int off = g.offset(l0 + lc);
+                const float2* src = base + off;
                 float sr = 0.f, si = 0.f;
                 int idx = 0;
                 for (int e = 0; e < n; ++e) {
-                    const float2 x = src[e * es];
+                    const float2 x = src[e * g.es];
                     const float2 w = tw[idx];
                     const float wy = sgn * w.y;
                     sr = fmaf(x.x, w.x, fmaf(-x.y, wy, sr));
@@ -131,7 +129,7 @@ __device__ void lds_dft_lines(float2* base, int nb, int bs, int nl, int ls, int 
                     if (idx >= n) idx -= n;
                 }
                 acc[i] = make_float2(sr, si);
-                addr[i] = b * bs + l * ls + k * es;
+                addr[i] = off + k * g.es;
             }
         }
         __syncthreads();
@@ -142,25 +140,52 @@ __device__ void lds_dft_lines(float2* base, int nb, int bs, int nl, int ls, int 
     __syncthreads();
 }
 
-// 2-D DFT (rows x cols, row stride cols) of nb arrays spaced bs apart.
-__device__ void lds_dft2(float2* buf, int nb, int bs, int rows, int cols, const float2* twR,
-                         const float2* twC, bool inverse) {
-    lds_dft_lines(buf, nb, bs, rows, cols, 1, cols, twC, inverse);  // along columns index
-    lds_dft_lines(buf, nb, bs, cols, 1, cols, rows, twR, inverse);  // along rows index
+// n-point transforms along lines.  FAM > 0: compiled FFTs for n = FAM * 2^k <= kMaxFamilyN;
+// FAM == 0 or any other n: generic DFT.
+template <int FAM, int K, bool INV>
+__device__ __forceinline__ bool try_family_fft(float2* base, const wstfft::Lines& g, int n,
+                                               const float2* tw) {
+    constexpr int NN = FAM << K;
+    if constexpr (FAM <= 0 || NN > wstfft::kMaxFamilyN) {
+        return false;
+    } else {
+        if constexpr (NN >= 2) {
+            if (n == NN) {
+                wstfft::fft_lines<NN, INV>(base, g, tw);
+                return true;
+            }
+        }
+        return try_family_fft<FAM, K + 1, INV>(base, g, n, tw);
+    }
+}
+
+template <int FAM, bool INV>
+__device__ void lds_fft_lines(float2* base, const wstfft::Lines g, int n, const float2* tw) {
+    if (!try_family_fft<FAM, 0, INV>(base, g, n, tw)) lds_dft_lines_generic(base, g, n, tw, INV);
+}
+
+// 2-D transform of nb (rows x cols) arrays with row stride ld (odd), spaced bs apart.
+// FM / FN: size families of the row count / column count.
+template <int FM, int FN, bool INV>
+__device__ void lds_fft2(float2* buf, int nb, int bs, int rows, int cols, int ld, const float2* twR,
+                         const float2* twC) {
+    lds_fft_lines<FN, INV>(buf, wstfft::Lines{nb, bs, rows, ld, 1}, cols, twC);   // along rows
+    lds_fft_lines<FM, INV>(buf, wstfft::Lines{nb, bs, cols, 1, ld}, rows, twR);   // along columns
 }
 
 // Separable phi low-pass evaluated at the kept output points (unpad folded in):
 //   S[b][a][c] = sum_p hM[(s(a+1) - p) mod rows] * sum_q hN[(s(c+1) - q) mod cols] * U[b][p][q]
-// U real (stored in .x).  tmp: nb*rows*oN floats, S: nb*oM*oN floats.  Ends with a barrier.
-__device__ void lds_lowpass(const float2* U, int nb, int bs, int rows, int cols, const float* hM,
-                            const float* hN, int s, int oM, int oN, float* tmp, float* S) {
+// U real (in .x), row stride ld.  tmp: nb*rows*oN floats, S: nb*oM*oN floats.  Ends with a barrier.
+__device__ void lds_lowpass(const float2* U, int nb, int bs, int rows, int cols, int ld,
+                            const float* hM, const float* hN, int s, int oM, int oN, float* tmp,
+                            float* S) {
     const int T = blockDim.x;
     const int tot1 = nb * rows * oN;
     for (int o = threadIdx.x; o < tot1; o += T) {
         const int c = o % oN;
         const int p = (o / oN) % rows;
         const int b = o / (oN * rows);
-        const float2* row = U + b * bs + p * cols;
+        const float2* row = U + b * bs + p * ld;
         int idx = s * (c + 1);
         float acc = 0.f;
         for (int q = 0; q < cols; ++q) {
@@ -187,7 +212,7 @@ __device__ void lds_lowpass(const float2* U, int nb, int bs, int rows, int cols,
     __syncthreads();
 }
 
-// Write nb coefficient maps (S: nb x oM x oN) of plane `img`, coefficient k0 + b.
+// Write nb coefficient maps (S: nb x oM x oN) of plane `img`, coefficient k0 + b*kstride.
 // pooled: out[img][k] = mean, out[img][K + k] = population std.
 __device__ void emit(const float* S, int nb, int k0, int kstride, long long img, int K, int oM,
                      int oN, float* out, int pooled) {
@@ -223,16 +248,19 @@ __device__ void load_tables(const DevParams& p, float2* tw_l, float* lp_l) {
     for (int i = threadIdx.x; i < p.lp_total; i += blockDim.x) lp_l[i] = p.lp[i];
 }
 
+__host__ __device__ inline int odd_ld(int n) { return n | 1; }
+
 // ------------------------------------------------------------------------------------------
 // k_prep: one workgroup per plane
 // ------------------------------------------------------------------------------------------
+template <int FM, int FN>
 __global__ void __launch_bounds__(512) k_prep(DevParams p, const float* __restrict__ in,
                                               long long img0, float2* __restrict__ xhat,
                                               float* __restrict__ out, int pooled) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int PM = p.PM, PN = p.PN, n = PM * PN;
+    const int PM = p.PM, PN = p.PN, n = PM * PN, ld = odd_ld(PN);
     float2* A = reinterpret_cast<float2*>(smem);
-    float2* tw_l = A + n;
+    float2* tw_l = A + PM * ld;
     float* lp_l = reinterpret_cast<float*>(tw_l + p.tw_total);
     float* tmp = lp_l + p.lp_total;                 // PM * oN
     float* S = tmp + PM * p.oN;                     // oM * oN
@@ -255,27 +283,34 @@ __global__ void __launch_bounds__(512) k_prep(DevParams p, const float* __restri
             sv = reflect_index(v - p.padLeft, p.N);
         }
         const float val = x[su * inN + sv];
-        A[o] = make_float2(val, 0.f);
+        A[u * ld + v] = make_float2(val, 0.f);
         part += val;
     }
     const float mean = block_sum(part, red) / n;  // contains the barrier after the gather
 
     // S0: low-pass at level 0, decimation 2^J
-    lds_lowpass(A, 1, 0, PM, PN, lp_l + p.lp_off[0], lp_l + p.lp_off[1], 1 << p.J, p.oM, p.oN,
+    lds_lowpass(A, 1, 0, PM, PN, ld, lp_l + p.lp_off[0], lp_l + p.lp_off[1], 1 << p.J, p.oM, p.oN,
                 tmp, S);
     emit(S, 1, 0, 1, img, p.K, p.oM, p.oN, out, pooled);
 
     // mean-centred forward DFT for the band-pass paths
-    for (int o = threadIdx.x; o < n; o += blockDim.x) A[o].x -= mean;
+    for (int o = threadIdx.x; o < n; o += blockDim.x) {
+        const int u = o / PN, v = o - (o / PN) * PN;
+        A[u * ld + v].x -= mean;
+    }
     __syncthreads();
-    lds_dft2(A, 1, 0, PM, PN, tw_l + p.tw_off[0], tw_l + p.tw_off[1], false);
+    lds_fft2<FM, FN, false>(A, 1, 0, PM, PN, ld, tw_l + p.tw_off[0], tw_l + p.tw_off[1]);
     float2* dst = xhat + local * n;
-    for (int o = threadIdx.x; o < n; o += blockDim.x) dst[o] = A[o];
+    for (int o = threadIdx.x; o < n; o += blockDim.x) {
+        const int u = o / PN, v = o - (o / PN) * PN;
+        dst[o] = A[u * ld + v];
+    }
 }
 
 // ------------------------------------------------------------------------------------------
 // k_order12: one workgroup per (plane, theta1) at fixed j1
 // ------------------------------------------------------------------------------------------
+template <int FM, int FN>
 __global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int nimg,
                                                  long long img0, const float2* __restrict__ xhat,
                                                  float* __restrict__ out, int pooled) {
@@ -291,13 +326,12 @@ __global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int
     const long long img = img0 + local;
 
     const int PM = p.PM, PN = p.PN;
-    const int nM1 = PM >> j1, nN1 = PN >> j1, n1 = nM1 * nN1;
+    const int nM1 = PM >> j1, nN1 = PN >> j1, n1 = nM1 * nN1, ld1 = odd_ld(nN1);
     const bool do2 = (p.max_order >= 2) && (j1 < J - 1);
-    const int nM2max = nM1 >> 1, nN2max = nN1 >> 1;
-    const int slot = do2 ? nM2max * nN2max : 0;
+    const int slot = do2 ? (nM1 >> 1) * odd_ld(nN1 >> 1) : 0;
 
     float2* A = reinterpret_cast<float2*>(smem);
-    float2* B = A + n1;
+    float2* B = A + nM1 * ld1;
     float2* tw_l = B + G * slot;
     float* lp_l = reinterpret_cast<float*>(tw_l + p.tw_total);
     float* tmp = lp_l + p.lp_total;                   // G * nM1 * oN
@@ -323,38 +357,42 @@ __global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int
                 ai = fmaf(xv.y, f, ai);
             }
         }
-        A[o] = make_float2(ar, ai);
+        A[u * ld1 + v] = make_float2(ar, ai);
     }
     __syncthreads();
 
     // 2. U1 = |ifft(.)| ; combined normalisation of fold-mean and ifft = 1 / (PM * PN)
-    lds_dft2(A, 1, 0, nM1, nN1, tw_l + p.tw_off[2 * j1], tw_l + p.tw_off[2 * j1 + 1], true);
+    lds_fft2<FM, FN, true>(A, 1, 0, nM1, nN1, ld1, tw_l + p.tw_off[2 * j1], tw_l + p.tw_off[2 * j1 + 1]);
     const float sc1 = 1.f / (static_cast<float>(PM) * static_cast<float>(PN));
     float part = 0.f;
     for (int o = threadIdx.x; o < n1; o += blockDim.x) {
-        const float2 z = A[o];
+        const int u = o / nN1, v = o - (o / nN1) * nN1;
+        const float2 z = A[u * ld1 + v];
         const float m = sqrtf(z.x * z.x + z.y * z.y) * sc1;
-        A[o] = make_float2(m, 0.f);
+        A[u * ld1 + v] = make_float2(m, 0.f);
         part += m;
     }
     const float mean1 = block_sum(part, red) / n1;
 
     // 3. S1 at level j1, decimation 2^(J-j1)
-    lds_lowpass(A, 1, 0, nM1, nN1, lp_l + p.lp_off[2 * j1], lp_l + p.lp_off[2 * j1 + 1],
+    lds_lowpass(A, 1, 0, nM1, nN1, ld1, lp_l + p.lp_off[2 * j1], lp_l + p.lp_off[2 * j1 + 1],
                 1 << (J - j1), p.oM, p.oN, tmp, S);
     const int n1idx = j1 * L + l1;
     emit(S, 1, 1 + n1idx, 1, img, p.K, p.oM, p.oN, out, pooled);
     if (!do2) return;
 
     // 4. U1hat = fft(U1 - mean) kept in LDS
-    for (int o = threadIdx.x; o < n1; o += blockDim.x) A[o].x -= mean1;
+    for (int o = threadIdx.x; o < n1; o += blockDim.x) {
+        const int u = o / nN1, v = o - (o / nN1) * nN1;
+        A[u * ld1 + v].x -= mean1;
+    }
     __syncthreads();
-    lds_dft2(A, 1, 0, nM1, nN1, tw_l + p.tw_off[2 * j1], tw_l + p.tw_off[2 * j1 + 1], false);
+    lds_fft2<FM, FN, false>(A, 1, 0, nM1, nN1, ld1, tw_l + p.tw_off[2 * j1], tw_l + p.tw_off[2 * j1 + 1]);
 
     const float sc2 = 1.f / static_cast<float>(n1);
     const int kbase = p.o2_base[n1idx];
     for (int j2 = j1 + 1; j2 < J; ++j2) {
-        const int nM2 = PM >> j2, nN2 = PN >> j2, n2 = nM2 * nN2;
+        const int nM2 = PM >> j2, nN2 = PN >> j2, n2 = nM2 * nN2, ld2 = odd_ld(nN2);
         const int s2 = 1 << (j2 - j1);
         for (int l2a = 0; l2a < L; l2a += G) {
             const int g = min(G, L - l2a);
@@ -366,33 +404,92 @@ __global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int
                 const float* ps = p.psi + p.psi_off[(j2 * L + l2a + b) * J + j1];
                 float ar = 0.f, ai = 0.f;
                 for (int i = 0; i < s2; ++i) {
-                    const int rowoff = (u + i * nM2) * nN1 + v;
+                    const int su = u + i * nM2;
                     for (int j = 0; j < s2; ++j) {
-                        const int idx = rowoff + j * nN2;
-                        const float f = ps[idx];
-                        const float2 xv = A[idx];
+                        const int sv = v + j * nN2;
+                        const float f = ps[su * nN1 + sv];
+                        const float2 xv = A[su * ld1 + sv];
                         ar = fmaf(xv.x, f, ar);
                         ai = fmaf(xv.y, f, ai);
                     }
                 }
-                B[b * slot + r] = make_float2(ar, ai);
+                B[b * slot + u * ld2 + v] = make_float2(ar, ai);
             }
             __syncthreads();
-            lds_dft2(B, g, slot, nM2, nN2, tw_l + p.tw_off[2 * j2], tw_l + p.tw_off[2 * j2 + 1],
-                     true);
+            lds_fft2<FM, FN, true>(B, g, slot, nM2, nN2, ld2, tw_l + p.tw_off[2 * j2],
+                           tw_l + p.tw_off[2 * j2 + 1]);
             for (int o = threadIdx.x; o < g * n2; o += blockDim.x) {
                 const int b = o / n2;
                 const int r = o - b * n2;
-                const float2 z = B[b * slot + r];
-                B[b * slot + r] = make_float2(sqrtf(z.x * z.x + z.y * z.y) * sc2, 0.f);
+                const int u = r / nN2, v = r - (r / nN2) * nN2;
+                const float2 z = B[b * slot + u * ld2 + v];
+                B[b * slot + u * ld2 + v] = make_float2(sqrtf(z.x * z.x + z.y * z.y) * sc2, 0.f);
             }
             __syncthreads();
-            lds_lowpass(B, g, slot, nM2, nN2, lp_l + p.lp_off[2 * j2], lp_l + p.lp_off[2 * j2 + 1],
-                        1 << (J - j2), p.oM, p.oN, tmp, S);
+            lds_lowpass(B, g, slot, nM2, nN2, ld2, lp_l + p.lp_off[2 * j2],
+                        lp_l + p.lp_off[2 * j2 + 1], 1 << (J - j2), p.oM, p.oN, tmp, S);
             emit(S, g, kbase + (j2 - j1 - 1) * L + l2a, 1, img, p.K, p.oM, p.oN, out, pooled);
             __syncthreads();
         }
     }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// size-family instantiations
+// ------------------------------------------------------------------------------------------
+#define WST_FAMILY_PAIRS(X) X(0, 0) X(1, 1) X(3, 3) X(5, 5) X(9, 9) X(17, 17) X(3, 1) X(1, 3)
+
+namespace {
+
+int odd_part(int n) {
+    while (n > 0 && (n % 2) == 0) n /= 2;
+    return n;
+}
+int family_of(int P) {
+    const int o = odd_part(P);
+    const bool compiled = (o == 1 || o == 3 || o == 5 || o == 9 || o == 17);
+    return (compiled && P <= wstfft::kMaxFamilyN) ? o : 0;
+}
+bool pair_compiled(int fm, int fn) {
+#define WST_PAIR_EQ(A, B) if (fm == A && fn == B) return true;
+    WST_FAMILY_PAIRS(WST_PAIR_EQ)
+#undef WST_PAIR_EQ
+    return false;
+}
+int set_lds_attributes() {
+#define WST_PAIR_ATTR(A, B)                                                                      \
+    WST_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_prep<A, B>),              \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));    \
+    WST_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_order12<A, B>),           \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));
+    WST_FAMILY_PAIRS(WST_PAIR_ATTR)
+#undef WST_PAIR_ATTR
+    return WST_OK;
+}
+void launch_prep(int fm, int fn, dim3 grid, dim3 block, size_t lds, hipStream_t st,
+                 const DevParams& dp, const float* in, long long img0, float2* xhat, float* out,
+                 int pooled) {
+#define WST_PAIR_PREP(A, B)                                                                      \
+    if (fm == A && fn == B) {                                                                    \
+        hipLaunchKernelGGL((k_prep<A, B>), grid, block, lds, st, dp, in, img0, xhat, out, pooled); \
+        return;                                                                                  \
+    }
+    WST_FAMILY_PAIRS(WST_PAIR_PREP)
+#undef WST_PAIR_PREP
+}
+void launch_order12(int fm, int fn, dim3 grid, dim3 block, size_t lds, hipStream_t st,
+                    const DevParams& dp, int j1, int G, int nimg, long long img0,
+                    const float2* xhat, float* out, int pooled) {
+#define WST_PAIR_O12(A, B)                                                                       \
+    if (fm == A && fn == B) {                                                                    \
+        hipLaunchKernelGGL((k_order12<A, B>), grid, block, lds, st, dp, j1, G, nimg, img0, xhat,  \
+                           out, pooled);                                                         \
+        return;                                                                                  \
+    }
+    WST_FAMILY_PAIRS(WST_PAIR_O12)
+#undef WST_PAIR_O12
 }
 
 }  // namespace
@@ -413,6 +510,7 @@ struct wst_plan {
     int* d_tw_off = nullptr;
     int* d_o2 = nullptr;
     // launch geometry
+    int fam_m = 0, fam_n = 0;   // FFT size families (odd part of PM / PN), 0 = generic DFT
     int prep_threads = 256;
     size_t prep_lds = 0;
     std::vector<int> k1_threads, k1_G;
@@ -542,7 +640,7 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     // --- LDS budgets ---
     const size_t tables = align16(tw.size() * sizeof(float2)) + align16(lp.size() * sizeof(float));
     const size_t P2 = static_cast<size_t>(g.PM) * g.PN;
-    plan->prep_lds = align16(P2 * sizeof(float2)) + tables +
+    plan->prep_lds = align16(static_cast<size_t>(g.PM) * (g.PN | 1) * sizeof(float2)) + tables +
                      align16((static_cast<size_t>(g.PM) * g.oN + g.oM * g.oN + 16) * sizeof(float));
     if (plan->prep_lds > static_cast<size_t>(kMaxLds))
         return fail(WST_ERR_UNSUPPORTED,
@@ -554,10 +652,11 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     plan->k1_lds.resize(J);
     for (int j1 = 0; j1 < J; ++j1) {
         const size_t n1 = static_cast<size_t>(g.PM >> j1) * (g.PN >> j1);
+        const size_t n1p = static_cast<size_t>(g.PM >> j1) * ((g.PN >> j1) | 1);
         const bool do2 = max_order >= 2 && j1 < J - 1;
-        const size_t slot = do2 ? static_cast<size_t>(g.PM >> (j1 + 1)) * (g.PN >> (j1 + 1)) : 0;
+        const size_t slot = do2 ? static_cast<size_t>(g.PM >> (j1 + 1)) * ((g.PN >> (j1 + 1)) | 1) : 0;
         auto lds_for = [&](int G) {
-            return align16(n1 * sizeof(float2)) + align16(G * slot * sizeof(float2)) + tables +
+            return align16(n1p * sizeof(float2)) + align16(G * slot * sizeof(float2)) + tables +
                    align16((static_cast<size_t>(G) * (g.PM >> j1) * g.oN +
                             static_cast<size_t>(G) * g.oM * g.oN + 16) * sizeof(float));
         };
@@ -570,10 +669,10 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
         plan->k1_lds[j1] = lds_for(G);
         plan->k1_threads[j1] = n1 >= 4096 ? 512 : 256;
     }
-    WST_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_prep),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));
-    WST_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_order12),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));
+    if ((rc = set_lds_attributes()) != WST_OK) return rc;
+    plan->fam_m = family_of(g.PM);
+    plan->fam_n = family_of(g.PN);
+    if (!pair_compiled(plan->fam_m, plan->fam_n)) plan->fam_m = plan->fam_n = 0;
     *out = plan.release();
     g_last_error.clear();
     return WST_OK;
@@ -687,16 +786,16 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
     for (int64_t c0 = 0; c0 < nbatch; c0 += chunk) {
         const int nimg = static_cast<int>(std::min<int64_t>(chunk, nbatch - c0));
         if ((rc = timer.begin(stream)) != WST_OK) return rc;
-        hipLaunchKernelGGL(k_prep, dim3(nimg), dim3(plan->prep_threads), plan->prep_lds, stream,
-                           plan->dp, d_in + c0 * inM * inN, static_cast<long long>(c0), xhat, d_out,
-                           pooled);
+        launch_prep(plan->fam_m, plan->fam_n, dim3(nimg), dim3(plan->prep_threads), plan->prep_lds,
+                    stream, plan->dp, d_in + c0 * inM * inN, static_cast<long long>(c0), xhat, d_out,
+                    pooled);
         WST_HIP_CHECK(hipGetLastError());
         if ((rc = timer.end(stream, 0)) != WST_OK) return rc;
         for (int j1 = 0; j1 < g.J; ++j1) {
             if ((rc = timer.begin(stream)) != WST_OK) return rc;
-            hipLaunchKernelGGL(k_order12, dim3(nimg * g.L), dim3(plan->k1_threads[j1]),
-                               plan->k1_lds[j1], stream, plan->dp, j1, plan->k1_G[j1], nimg,
-                               static_cast<long long>(c0), xhat, d_out, pooled);
+            launch_order12(plan->fam_m, plan->fam_n, dim3(nimg * g.L), dim3(plan->k1_threads[j1]),
+                           plan->k1_lds[j1], stream, plan->dp, j1, plan->k1_G[j1], nimg,
+                           static_cast<long long>(c0), xhat, d_out, pooled);
             WST_HIP_CHECK(hipGetLastError());
             if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
         }
@@ -759,6 +858,51 @@ int wst_host_filter(int M, int N, int J, int L, int kind, int j, int l, int r, d
         std::memcpy(out, v.data(), v.size() * sizeof(double));
     } catch (const std::exception& e) {
         return fail(WST_ERR_UNSUPPORTED, e.what());
+    }
+    return WST_OK;
+}
+
+int wst_host_fft_lines(int n, int inverse, float* data, int nb, int bs, int nl, int ls, int es,
+                       int threads) {
+    if (!data || n < 1 || nb < 1 || nl < 1 || threads < 1) return fail(WST_ERR_INVALID, "bad arguments");
+    std::vector<float2> tw(static_cast<size_t>(n));
+    for (int k = 0; k < n; ++k) {
+        const double a = 2.0 * 3.14159265358979323846 * k / n;
+        tw[k] = make_float2(static_cast<float>(std::cos(a)), static_cast<float>(-std::sin(a)));
+    }
+    float2* base = reinterpret_cast<float2*>(data);
+    const wstfft::Lines g{nb, bs, nl, ls, es};
+    switch (n) {
+#define WST_HOST_CASE(NN)                                                          \
+    case NN:                                                                       \
+        if (inverse) wstfft::fft_lines_host<NN, true>(base, g, tw.data(), threads); \
+        else wstfft::fft_lines_host<NN, false>(base, g, tw.data(), threads);        \
+        return WST_OK;
+        WST_FFT_SIZES(WST_HOST_CASE)
+#undef WST_HOST_CASE
+        default:
+            break;
+    }
+    // generic DFT, same arithmetic as lds_dft_lines_generic
+    const float sgn = inverse ? -1.f : 1.f;
+    std::vector<float2> line(static_cast<size_t>(n));
+    for (int L0 = 0; L0 < g.nlines(); ++L0) {
+        const int off = g.offset(L0);
+        for (int e = 0; e < n; ++e) line[e] = base[off + e * es];
+        for (int k = 0; k < n; ++k) {
+            float sr = 0.f, si = 0.f;
+            int idx = 0;
+            for (int e = 0; e < n; ++e) {
+                const float2 x = line[e];
+                const float2 w = tw[idx];
+                const float wy = sgn * w.y;
+                sr = std::fma(x.x, w.x, std::fma(-x.y, wy, sr));
+                si = std::fma(x.x, wy, std::fma(x.y, w.x, si));
+                idx += k;
+                if (idx >= n) idx -= n;
+            }
+            base[off + k * es] = make_float2(sr, si);
+        }
     }
     return WST_OK;
 }
