@@ -1,0 +1,30 @@
+"""Timing ablation of k_order12 phases (dev tool): per WST_DEBUG_SKIP mask, per-kernel ms."""
+import os, subprocess, sys, json
+masks = {"full": 0, "no_o1_fold": 128, "no_o1_ifft": 1, "no_S1": 2, "no_U1_fft": 4, "no_o2_fold": 8,
+         "no_o2_ifft": 16, "no_o2_mod": 32, "no_o2_lowpass": 64, "no_order2_all": 8 | 16 | 32 | 64,
+         "only_o2_ifft": 1 | 2 | 4 | 8 | 32 | 64 | 128}
+child = r'''
+import os, sys, json
+sys.path.insert(0, os.getcwd())
+import numpy as np, torch, wst_amd
+from wst_amd import _lib
+B=3072
+x = torch.from_numpy(np.random.default_rng(1).integers(0,256,(B,64,64),dtype=np.uint8).astype(np.float32)/255).cuda()
+plan = _lib.Plan(64,64,4,8)
+out = torch.empty((B, plan.K, 4, 4), device="cuda")
+wsb = plan.workspace_bytes(2048); ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+st = torch.cuda.current_stream().cuda_stream
+for _ in range(2): plan.forward(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st)
+acc = [0.0]*5
+for _ in range(3):
+    ms = plan.forward_profiled(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st, 5)
+    acc = [a+b for a,b in zip(acc, ms)]
+print(json.dumps([a/3 for a in acc]))
+'''
+res = {}
+for name, m in masks.items():
+    env = dict(os.environ, WST_DEBUG_SKIP=str(m))
+    r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=300)
+    line = [l for l in r.stdout.splitlines() if l.startswith("[")]
+    res[name] = json.loads(line[-1]) if line else r.stderr[-300:]
+    print(name, res[name], flush=True)

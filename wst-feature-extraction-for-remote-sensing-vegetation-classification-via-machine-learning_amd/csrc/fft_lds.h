@@ -225,6 +225,11 @@ struct Lines {
     }
 };
 
+// Epilogue applied to every value of a line transform's final store (e.g. |.| * scale).
+struct EpiIdentity {
+    WST_HD float2 operator()(float2 v) const { return v; }
+};
+
 template <int N, bool INV>
 struct LineFFT {
     static constexpr int N2 = split_n2(N);
@@ -232,7 +237,8 @@ struct LineFFT {
     static constexpr int UPT = (N2 <= 4) ? 4 : (N2 <= 8 ? 2 : 1);  // stage-B units per thread
 
     // single stage: unit = whole line
-    static WST_HD void single_unit(float2* base, const Lines& g, int u) {
+    template <class Epi>
+    static WST_HD void single_unit(float2* base, const Lines& g, int u, Epi& epi) {
         float2* p = base + g.offset(u);
         float2 v[N];
         static_for<0, N>([&](auto ec) {
@@ -242,7 +248,7 @@ struct LineFFT {
         rfft<N, INV>(v);
         static_for<0, N>([&](auto ec) {
             constexpr int e = decltype(ec)::value;
-            p[e * g.es] = v[e];
+            p[e * g.es] = epi(v[e]);
         });
     }
     // stage A: unit u -> (line = u % nlines, n2 = u / nlines)
@@ -280,11 +286,13 @@ struct LineFFT {
         rfft<N2, INV>(v);
         return lb + k1 * g.es;
     }
-    static WST_HD void stageB_store(float2* base, const Lines& g, int addr, const float2 (&v)[N2]) {
+    template <class Epi>
+    static WST_HD void stageB_store(float2* base, const Lines& g, int addr, const float2 (&v)[N2],
+                                    Epi& epi) {
         float2* q = base + addr;
         static_for<0, N2>([&](auto ec) {
             constexpr int e = decltype(ec)::value;
-            q[e * N1 * g.es] = v[e];
+            q[e * N1 * g.es] = epi(v[e]);
         });
     }
     static WST_HD int lines_per_round(int T) {
@@ -295,13 +303,13 @@ struct LineFFT {
 
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
 // Device driver.  Ends with a barrier.
-template <int N, bool INV>
-__device__ void fft_lines(float2* base, const Lines g, const float2* tw) {
+template <int N, bool INV, class Epi = EpiIdentity>
+__device__ void fft_lines(float2* base, const Lines g, const float2* tw, Epi& epi) {
     using F = LineFFT<N, INV>;
     const int T = blockDim.x;
     const int nlines = g.nlines();
     if constexpr (F::N2 == 1) {
-        for (int u = threadIdx.x; u < nlines; u += T) F::single_unit(base, g, u);
+        for (int u = threadIdx.x; u < nlines; u += T) F::single_unit(base, g, u, epi);
         __syncthreads();
     } else {
         const int unitsA = nlines * F::N2;
@@ -321,7 +329,7 @@ __device__ void fft_lines(float2* base, const Lines g, const float2* tw) {
             __syncthreads();
             static_for<0, F::UPT>([&](auto ic) {
                 constexpr int i = decltype(ic)::value;
-                if (addr[i] >= 0) F::stageB_store(base, g, addr[i], v[i]);
+                if (addr[i] >= 0) F::stageB_store(base, g, addr[i], v[i], epi);
             });
         }
         __syncthreads();
@@ -333,9 +341,10 @@ __device__ void fft_lines(float2* base, const Lines g, const float2* tw) {
 template <int N, bool INV>
 inline void fft_lines_host(float2* base, const Lines g, const float2* tw, int T) {
     using F = LineFFT<N, INV>;
+    EpiIdentity epi;
     const int nlines = g.nlines();
     if constexpr (F::N2 == 1) {
-        for (int u = 0; u < nlines; ++u) F::single_unit(base, g, u);
+        for (int u = 0; u < nlines; ++u) F::single_unit(base, g, u, epi);
     } else {
         for (int u = 0; u < nlines * F::N2; ++u) F::stageA_unit(base, g, tw, u);
         const int lpr = F::lines_per_round(T);
@@ -352,7 +361,7 @@ inline void fft_lines_host(float2* base, const Lines g, const float2* tw, int T)
             for (int w = 0; w < units; ++w) {
                 float2 tmp[F::N2];
                 for (int e = 0; e < F::N2; ++e) tmp[e] = v[static_cast<size_t>(w) * F::N2 + e];
-                F::stageB_store(base, g, addr[w], tmp);
+                F::stageB_store(base, g, addr[w], tmp, epi);
             }
             delete[] v;
             delete[] addr;

@@ -24,6 +24,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -60,6 +61,7 @@ struct DevParams {
     int M, N, PM, PN, J, L, max_order, pre_pad, K;
     int mM, mN, oM, oN, padTop, padLeft;
     int tw_total, lp_total;       // element counts of the twiddle / low-pass pools
+    int dbg_skip;                 // timing-ablation mask (env WST_DEBUG_SKIP; 0 in production)
     const float* psi;             // concatenated psi Fourier levels (fp32)
     const long long* psi_off;     // [(j*L + l)*J + r]
     const float* lp;              // concatenated spatial low-pass taps hM[r], hN[r]
@@ -67,6 +69,8 @@ struct DevParams {
     const float2* tw;             // concatenated twiddle tables exp(-2 pi i k / n)
     const int* tw_off;            // [2r] -> n = PM>>r, [2r+1] -> n = PN>>r, r in [0, J]
     const int* o2_base;           // first order-2 coefficient of each n1 = j1*L + l1
+    const float4* psi4;           // order-2 filters, 4 consecutive l2 interleaved per bin
+    const long long* psi4_off;    // [(j2*J + r)*ceil(L/4) + q] -> level r of l2 in [4q, 4q+4)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -93,10 +97,22 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
     return s;
 }
 
+// |z| * scale stored as a real value; optionally accumulates the per-thread sum (for means)
+struct EpiModulus {
+    float scale;
+    float sum;
+    __device__ float2 operator()(float2 z) {
+        const float m = sqrtf(fmaf(z.x, z.x, z.y * z.y)) * scale;
+        sum += m;
+        return make_float2(m, 0.f);
+    }
+};
+
 // Generic O(n) DFT along lines (fallback for sizes without a compiled FFT).  Lines are processed
 // in chunks of whole lines that fit the register tile: read phase -> barrier -> write phase.
+template <class Epi>
 __device__ void lds_dft_lines_generic(float2* base, const wstfft::Lines g, int n, const float2* tw,
-                                      bool inverse) {
+                                      bool inverse, Epi& epi) {
     const int T = blockDim.x;
     const int lines_total = g.nlines();
     int lpc = (T * kMaxO) / n;
@@ -135,64 +151,81 @@ __device__ void lds_dft_lines_generic(float2* base, const wstfft::Lines g, int n
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < kMaxO; ++i)
-            if (addr[i] >= 0) base[addr[i]] = acc[i];
+            if (addr[i] >= 0) base[addr[i]] = epi(acc[i]);
     }
     __syncthreads();
 }
 
 // n-point transforms along lines.  FAM > 0: compiled FFTs for n = FAM * 2^k <= kMaxFamilyN;
 // FAM == 0 or any other n: generic DFT.
-template <int FAM, int K, bool INV>
-__device__ __forceinline__ bool try_family_fft(float2* base, const wstfft::Lines& g, int n,
-                                               const float2* tw) {
+// n-point transforms along lines.  FAM > 0: the compiled FFTs n = FAM * 2^k <= MAXN (a plan's
+// level sizes always belong to its family, so no fallback is compiled into these kernels);
+// FAM == 0: generic DFT for any n.
+template <int FAM, int K, int MAXN, bool INV, class Epi>
+__device__ __forceinline__ void family_fft(float2* base, const wstfft::Lines& g, int n,
+                                           const float2* tw, Epi& epi) {
     constexpr int NN = FAM << K;
-    if constexpr (FAM <= 0 || NN > wstfft::kMaxFamilyN) {
-        return false;
-    } else {
+    if constexpr (NN <= MAXN && NN <= wstfft::kMaxFamilyN) {
         if constexpr (NN >= 2) {
             if (n == NN) {
-                wstfft::fft_lines<NN, INV>(base, g, tw);
-                return true;
+                wstfft::fft_lines<NN, INV>(base, g, tw, epi);
+                return;
             }
         }
-        return try_family_fft<FAM, K + 1, INV>(base, g, n, tw);
+        family_fft<FAM, K + 1, MAXN, INV>(base, g, n, tw, epi);
     }
 }
 
-template <int FAM, bool INV>
-__device__ void lds_fft_lines(float2* base, const wstfft::Lines g, int n, const float2* tw) {
-    if (!try_family_fft<FAM, 0, INV>(base, g, n, tw)) lds_dft_lines_generic(base, g, n, tw, INV);
+template <int FAM, int MAXN, bool INV, class Epi>
+__device__ void lds_fft_lines(float2* base, const wstfft::Lines g, int n, const float2* tw, Epi& epi) {
+    if constexpr (FAM > 0)
+        family_fft<FAM, 0, MAXN, INV>(base, g, n, tw, epi);
+    else
+        lds_dft_lines_generic(base, g, n, tw, INV, epi);
 }
 
-// 2-D transform of nb (rows x cols) arrays with row stride ld (odd), spaced bs apart.
-// FM / FN: size families of the row count / column count.
-template <int FM, int FN, bool INV>
+// 2-D transform of nb (rows x cols) arrays with row stride ld (odd), spaced bs apart; `epi` is
+// applied to the final (column-pass) stores.  FM / FN: size families of rows / cols; MAXN caps
+// the compiled sizes (smaller caps -> fewer registers for the small-level kernels).
+template <int FM, int FN, int MAXN, bool INV, class Epi>
 __device__ void lds_fft2(float2* buf, int nb, int bs, int rows, int cols, int ld, const float2* twR,
-                         const float2* twC) {
-    lds_fft_lines<FN, INV>(buf, wstfft::Lines{nb, bs, rows, ld, 1}, cols, twC);   // along rows
-    lds_fft_lines<FM, INV>(buf, wstfft::Lines{nb, bs, cols, 1, ld}, rows, twR);   // along columns
+                         const float2* twC, Epi& epi) {
+    wstfft::EpiIdentity id;
+    lds_fft_lines<FN, MAXN, INV>(buf, wstfft::Lines{nb, bs, rows, ld, 1}, cols, twC, id);  // rows
+    lds_fft_lines<FM, MAXN, INV>(buf, wstfft::Lines{nb, bs, cols, 1, ld}, rows, twR, epi); // cols
 }
 
 // Separable phi low-pass evaluated at the kept output points (unpad folded in):
-//   S[b][a][c] = sum_p hM[(s(a+1) - p) mod rows] * sum_q hN[(s(c+1) - q) mod cols] * U[b][p][q]
-// U real (in .x), row stride ld.  tmp: nb*rows*oN floats, S: nb*oM*oN floats.  Ends with a barrier.
-__device__ void lds_lowpass(const float2* U, int nb, int bs, int rows, int cols, int ld,
-                            const float* hM, const float* hN, int s, int oM, int oN, float* tmp,
-                            float* S) {
+//   S[b][a][c] = sum_p hM[s(a+1) - p] * sum_q hN[s(c+1) - q] * U[b][p][q]   (indices mod n)
+// hM2 / hN2 are the taps stored twice (length 2n) so s(c+1) + n - q never wraps.  U real (.x),
+// row stride ld.  tmp: nb*rows*oN floats, S: nb*oM*oN floats.  Step 1 computes OW output columns
+// per pass over a row (oN > OW: several passes).  Ends with a barrier.
+template <int OW>
+__device__ void lds_lowpass_t(const float2* U, int nb, int bs, int rows, int cols, int ld,
+                              const float* hM2, const float* hN2, int s, int oM, int oN, float* tmp,
+                              float* S) {
     const int T = blockDim.x;
-    const int tot1 = nb * rows * oN;
-    for (int o = threadIdx.x; o < tot1; o += T) {
-        const int c = o % oN;
-        const int p = (o / oN) % rows;
-        const int b = o / (oN * rows);
+    const int nchunk = (oN + OW - 1) / OW;
+    for (int it = threadIdx.x; it < nb * rows * nchunk; it += T) {
+        const int ch = it % nchunk;
+        const int bp = it / nchunk;
+        const int b = bp / rows;
+        const int p = bp - b * rows;
+        const int c0 = ch * OW;
         const float2* row = U + b * bs + p * ld;
-        int idx = s * (c + 1);
-        float acc = 0.f;
+        float acc[OW];
+#pragma unroll
+        for (int c = 0; c < OW; ++c) acc[c] = 0.f;
+        const float* h0 = hN2 + cols + s * (c0 + 1);   // tap index s(c+1) + cols - q
+#pragma unroll 4
         for (int q = 0; q < cols; ++q) {
-            acc = fmaf(row[q].x, hN[idx], acc);
-            idx = (idx == 0) ? cols - 1 : idx - 1;
+            const float x = row[q].x;
+#pragma unroll
+            for (int c = 0; c < OW; ++c) acc[c] = fmaf(x, h0[s * c - q], acc[c]);
         }
-        tmp[o] = acc;
+#pragma unroll
+        for (int c = 0; c < OW; ++c)
+            if (c0 + c < oN) tmp[bp * oN + c0 + c] = acc[c];
     }
     __syncthreads();
     const int tot2 = nb * oM * oN;
@@ -201,15 +234,27 @@ __device__ void lds_lowpass(const float2* U, int nb, int bs, int rows, int cols,
         const int a = (o / oN) % oM;
         const int b = o / (oN * oM);
         const float* t = tmp + b * rows * oN + c;
-        int idx = s * (a + 1);
-        float acc = 0.f;
-        for (int p = 0; p < rows; ++p) {
-            acc = fmaf(hM[idx], t[p * oN], acc);
-            idx = (idx == 0) ? rows - 1 : idx - 1;
+        const float* h = hM2 + rows + s * (a + 1);
+        float acc0 = 0.f, acc1 = 0.f;
+        int p = 0;
+#pragma unroll 4
+        for (; p + 1 < rows; p += 2) {
+            acc0 = fmaf(h[-p], t[p * oN], acc0);
+            acc1 = fmaf(h[-p - 1], t[(p + 1) * oN], acc1);
         }
-        S[o] = acc;
+        if (p < rows) acc0 = fmaf(h[-p], t[p * oN], acc0);
+        S[o] = acc0 + acc1;
     }
     __syncthreads();
+}
+
+__device__ void lds_lowpass(const float2* U, int nb, int bs, int rows, int cols, int ld,
+                            const float* hM2, const float* hN2, int s, int oM, int oN, float* tmp,
+                            float* S) {
+    if (oN <= 4)
+        lds_lowpass_t<4>(U, nb, bs, rows, cols, ld, hM2, hN2, s, oM, oN, tmp, S);
+    else
+        lds_lowpass_t<8>(U, nb, bs, rows, cols, ld, hM2, hN2, s, oM, oN, tmp, S);
 }
 
 // Write nb coefficient maps (S: nb x oM x oN) of plane `img`, coefficient k0 + b*kstride.
@@ -249,6 +294,99 @@ __device__ void load_tables(const DevParams& p, float2* tw_l, float* lp_l) {
 }
 
 __host__ __device__ inline int odd_ld(int n) { return n | 1; }
+
+// Order-2 fold of one group of (up to) 4 paths:
+//   B_b[u][v] = sum_{i,j < S} A[u + i nM2][v + j nN2] * psi_b[u + i nM2][v + j nN2]
+// A: U1hat (stride ld1), psi4: the 4 paths' filters interleaved per bin (float4, dense nN1 rows).
+template <int S>
+__device__ void fold4(const float2* A, int ld1, int nN1, const float4* __restrict__ psi4, float2* B,
+                      int slot, int ld2, int nM2, int nN2, int g) {
+    const int items = nM2 * nN2;
+    for (int it = threadIdx.x; it < items; it += blockDim.x) {
+        const int u = it / nN2, v = it - (it / nN2) * nN2;
+        float2 acc[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[b] = make_float2(0.f, 0.f);
+#pragma unroll(S <= 4 ? S : 1)
+        for (int i = 0; i < S; ++i) {
+            const int su = u + i * nM2;
+            const float2* arow = A + su * ld1 + v;
+            const float4* frow = psi4 + su * nN1 + v;
+#pragma unroll(S <= 8 ? S : 8)
+            for (int j = 0; j < S; ++j) {
+                const float2 a = arow[j * nN2];
+                const float4 f = frow[j * nN2];
+                acc[0] = make_float2(fmaf(a.x, f.x, acc[0].x), fmaf(a.y, f.x, acc[0].y));
+                acc[1] = make_float2(fmaf(a.x, f.y, acc[1].x), fmaf(a.y, f.y, acc[1].y));
+                acc[2] = make_float2(fmaf(a.x, f.z, acc[2].x), fmaf(a.y, f.z, acc[2].y));
+                acc[3] = make_float2(fmaf(a.x, f.w, acc[3].x), fmaf(a.y, f.w, acc[3].y));
+            }
+        }
+        float2* dst = B + u * ld2 + v;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+            if (b < g) dst[b * slot] = acc[b];
+    }
+}
+
+__device__ void fold4_any(int s2, const float2* A, int ld1, int nN1, const float4* psi4, float2* B,
+                          int slot, int ld2, int nM2, int nN2, int g) {
+    switch (s2) {
+        case 2: fold4<2>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g); break;
+        case 4: fold4<4>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g); break;
+        case 8: fold4<8>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g); break;
+        case 16: fold4<16>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g); break;
+        case 32: fold4<32>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g); break;
+        default: fold4<64>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g); break;
+    }
+}
+
+// Order-1 fold from HBM/L2: A[u][v] = sum_{i,j < S} X[u + i nM1][v + j nN1] * psi0[...]
+template <int S>
+__device__ void fold1(const float2* __restrict__ X, const float* __restrict__ psi0, int PN, float2* A,
+                      int ld1, int nM1, int nN1) {
+    const int items = nM1 * nN1;
+    const int T = blockDim.x;
+    constexpr int U = (S == 1) ? 4 : (S == 2 ? 2 : 1);   // items per thread in flight
+    for (int it0 = threadIdx.x; it0 < items; it0 += U * T) {
+        float2 acc[U];
+        int dst[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int it = it0 + k * T;
+            acc[k] = make_float2(0.f, 0.f);
+            dst[k] = -1;
+            if (it < items) {
+                const int u = it / nN1, v = it - (it / nN1) * nN1;
+                dst[k] = u * ld1 + v;
+#pragma unroll
+                for (int i = 0; i < S; ++i) {
+#pragma unroll
+                    for (int j = 0; j < S; ++j) {
+                        const int idx = (u + i * nM1) * PN + v + j * nN1;
+                        const float f = psi0[idx];
+                        const float2 xv = X[idx];
+                        acc[k] = make_float2(fmaf(xv.x, f, acc[k].x), fmaf(xv.y, f, acc[k].y));
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            if (dst[k] >= 0) A[dst[k]] = acc[k];
+    }
+}
+
+__device__ void fold1_any(int s1, const float2* X, const float* psi0, int PN, float2* A, int ld1,
+                          int nM1, int nN1) {
+    switch (s1) {
+        case 1: fold1<1>(X, psi0, PN, A, ld1, nM1, nN1); break;
+        case 2: fold1<2>(X, psi0, PN, A, ld1, nM1, nN1); break;
+        case 4: fold1<4>(X, psi0, PN, A, ld1, nM1, nN1); break;
+        case 8: fold1<8>(X, psi0, PN, A, ld1, nM1, nN1); break;
+        default: fold1<16>(X, psi0, PN, A, ld1, nM1, nN1); break;
+    }
+}
 
 // ------------------------------------------------------------------------------------------
 // k_prep: one workgroup per plane
@@ -299,7 +437,9 @@ __global__ void __launch_bounds__(512) k_prep(DevParams p, const float* __restri
         A[u * ld + v].x -= mean;
     }
     __syncthreads();
-    lds_fft2<FM, FN, false>(A, 1, 0, PM, PN, ld, tw_l + p.tw_off[0], tw_l + p.tw_off[1]);
+    wstfft::EpiIdentity id;
+    lds_fft2<FM, FN, wstfft::kMaxFamilyN, false>(A, 1, 0, PM, PN, ld, tw_l + p.tw_off[0],
+                                                 tw_l + p.tw_off[1], id);
     float2* dst = xhat + local * n;
     for (int o = threadIdx.x; o < n; o += blockDim.x) {
         const int u = o / PN, v = o - (o / PN) * PN;
@@ -310,8 +450,8 @@ __global__ void __launch_bounds__(512) k_prep(DevParams p, const float* __restri
 // ------------------------------------------------------------------------------------------
 // k_order12: one workgroup per (plane, theta1) at fixed j1
 // ------------------------------------------------------------------------------------------
-template <int FM, int FN>
-__global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int nimg,
+template <int FM, int FN, int MAXN>
+__global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int tmpN, int nimg,
                                                  long long img0, const float2* __restrict__ xhat,
                                                  float* __restrict__ out, int pooled) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -334,51 +474,33 @@ __global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int
     float2* B = A + nM1 * ld1;
     float2* tw_l = B + G * slot;
     float* lp_l = reinterpret_cast<float*>(tw_l + p.tw_total);
-    float* tmp = lp_l + p.lp_total;                   // G * nM1 * oN
-    float* S = tmp + G * nM1 * p.oN;                  // G * oM * oN
-    float* red = S + G * p.oM * p.oN;                 // 16
+    float* tmp = lp_l + p.lp_total;                   // tmpN floats (host-sized low-pass scratch)
+    float* S = tmp + tmpN;                            // <= max(G, L) * oM * oN
+    float* red = S + max(G, L) * p.oM * p.oN;         // 16
 
     load_tables(p, tw_l, lp_l);
+    const int dbg = p.dbg_skip;
 
     // 1. fold_{2^j1}(Xhat * psi0_{j1,l1}) straight from HBM/L2
     const float* psi0 = p.psi + p.psi_off[(j1 * L + l1) * J + 0];
     const float2* X = xhat + static_cast<long long>(local) * PM * PN;
-    const int s1 = 1 << j1;
-    for (int o = threadIdx.x; o < n1; o += blockDim.x) {
-        const int u = o / nN1, v = o - (o / nN1) * nN1;
-        float ar = 0.f, ai = 0.f;
-        for (int i = 0; i < s1; ++i) {
-            const int rowoff = (u + i * nM1) * PN + v;
-            for (int j = 0; j < s1; ++j) {
-                const int idx = rowoff + j * nN1;
-                const float f = psi0[idx];
-                const float2 xv = X[idx];
-                ar = fmaf(xv.x, f, ar);
-                ai = fmaf(xv.y, f, ai);
-            }
-        }
-        A[u * ld1 + v] = make_float2(ar, ai);
-    }
+    if (!(dbg & 128)) fold1_any(1 << j1, X, psi0, PN, A, ld1, nM1, nN1);
     __syncthreads();
 
-    // 2. U1 = |ifft(.)| ; combined normalisation of fold-mean and ifft = 1 / (PM * PN)
-    lds_fft2<FM, FN, true>(A, 1, 0, nM1, nN1, ld1, tw_l + p.tw_off[2 * j1], tw_l + p.tw_off[2 * j1 + 1]);
-    const float sc1 = 1.f / (static_cast<float>(PM) * static_cast<float>(PN));
-    float part = 0.f;
-    for (int o = threadIdx.x; o < n1; o += blockDim.x) {
-        const int u = o / nN1, v = o - (o / nN1) * nN1;
-        const float2 z = A[u * ld1 + v];
-        const float m = sqrtf(z.x * z.x + z.y * z.y) * sc1;
-        A[u * ld1 + v] = make_float2(m, 0.f);
-        part += m;
-    }
-    const float mean1 = block_sum(part, red) / n1;
+    // 2. U1 = |ifft(.)| fused into the last FFT pass; normalisation of fold-mean + ifft = 1/(PM PN)
+    EpiModulus mod1{1.f / (static_cast<float>(PM) * static_cast<float>(PN)), 0.f};
+    if (!(dbg & 1))
+        lds_fft2<FM, FN, MAXN, true>(A, 1, 0, nM1, nN1, ld1, tw_l + p.tw_off[2 * j1],
+                                     tw_l + p.tw_off[2 * j1 + 1], mod1);
+    const float mean1 = block_sum(mod1.sum, red) / n1;
 
     // 3. S1 at level j1, decimation 2^(J-j1)
-    lds_lowpass(A, 1, 0, nM1, nN1, ld1, lp_l + p.lp_off[2 * j1], lp_l + p.lp_off[2 * j1 + 1],
-                1 << (J - j1), p.oM, p.oN, tmp, S);
     const int n1idx = j1 * L + l1;
-    emit(S, 1, 1 + n1idx, 1, img, p.K, p.oM, p.oN, out, pooled);
+    if (!(dbg & 2)) {
+        lds_lowpass(A, 1, 0, nM1, nN1, ld1, lp_l + p.lp_off[2 * j1], lp_l + p.lp_off[2 * j1 + 1],
+                    1 << (J - j1), p.oM, p.oN, tmp, S);
+        emit(S, 1, 1 + n1idx, 1, img, p.K, p.oM, p.oN, out, pooled);
+    }
     if (!do2) return;
 
     // 4. U1hat = fft(U1 - mean) kept in LDS
@@ -387,48 +509,44 @@ __global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int
         A[u * ld1 + v].x -= mean1;
     }
     __syncthreads();
-    lds_fft2<FM, FN, false>(A, 1, 0, nM1, nN1, ld1, tw_l + p.tw_off[2 * j1], tw_l + p.tw_off[2 * j1 + 1]);
+    wstfft::EpiIdentity id;
+    if (!(dbg & 4))
+        lds_fft2<FM, FN, MAXN, false>(A, 1, 0, nM1, nN1, ld1, tw_l + p.tw_off[2 * j1],
+                                      tw_l + p.tw_off[2 * j1 + 1], id);
 
-    const float sc2 = 1.f / static_cast<float>(n1);
     const int kbase = p.o2_base[n1idx];
+    const int nq = (L + 3) >> 2;
+    const int bcap = G * slot;   // complex capacity of the B region
     for (int j2 = j1 + 1; j2 < J; ++j2) {
-        const int nM2 = PM >> j2, nN2 = PN >> j2, n2 = nM2 * nN2, ld2 = odd_ld(nN2);
+        const int nM2 = PM >> j2, nN2 = PN >> j2, ld2 = odd_ld(nN2);
+        const int pslot = nM2 * ld2;                   // one path's array at this level
         const int s2 = 1 << (j2 - j1);
-        for (int l2a = 0; l2a < L; l2a += G) {
-            const int g = min(G, L - l2a);
-            // fold_{2^(j2-j1)}(U1hat * psi^{j1}_{j2,l2})
-            for (int o = threadIdx.x; o < g * n2; o += blockDim.x) {
-                const int b = o / n2;
-                const int r = o - b * n2;
-                const int u = r / nN2, v = r - (r / nN2) * nN2;
-                const float* ps = p.psi + p.psi_off[(j2 * L + l2a + b) * J + j1];
-                float ar = 0.f, ai = 0.f;
-                for (int i = 0; i < s2; ++i) {
-                    const int su = u + i * nM2;
-                    for (int j = 0; j < s2; ++j) {
-                        const int sv = v + j * nN2;
-                        const float f = ps[su * nN1 + sv];
-                        const float2 xv = A[su * ld1 + sv];
-                        ar = fmaf(xv.x, f, ar);
-                        ai = fmaf(xv.y, f, ai);
-                    }
+        int qpb = bcap / (4 * pslot);                  // 4-groups per batch
+        qpb = max(1, min(qpb, nq));
+        for (int q0 = 0; q0 < nq; q0 += qpb) {
+            const int nqb = min(qpb, nq - q0);
+            const int npath = min(4 * nqb, L - 4 * q0);
+            // 5. fold_{2^(j2-j1)}(U1hat * psi^{j1}_{j2, l2}) for every path of the batch
+            if (!(dbg & 8))
+                for (int qq = 0; qq < nqb; ++qq) {
+                    const int q = q0 + qq;
+                    const float4* ps4 = p.psi4 + p.psi4_off[(j2 * J + j1) * nq + q];
+                    fold4_any(s2, A, ld1, nN1, ps4, B + qq * 4 * pslot, pslot, ld2, nM2, nN2,
+                              min(4, L - 4 * q));
                 }
-                B[b * slot + u * ld2 + v] = make_float2(ar, ai);
-            }
             __syncthreads();
-            lds_fft2<FM, FN, true>(B, g, slot, nM2, nN2, ld2, tw_l + p.tw_off[2 * j2],
-                           tw_l + p.tw_off[2 * j2 + 1]);
-            for (int o = threadIdx.x; o < g * n2; o += blockDim.x) {
-                const int b = o / n2;
-                const int r = o - b * n2;
-                const int u = r / nN2, v = r - (r / nN2) * nN2;
-                const float2 z = B[b * slot + u * ld2 + v];
-                B[b * slot + u * ld2 + v] = make_float2(sqrtf(z.x * z.x + z.y * z.y) * sc2, 0.f);
+            // 6. U2 = |ifft(.)| (modulus fused), scale 1/(nM1 nN1)
+            EpiModulus mod2{1.f / static_cast<float>(n1), 0.f};
+            if (!(dbg & 16))
+                lds_fft2<FM, FN, MAXN, true>(B, npath, pslot, nM2, nN2, ld2, tw_l + p.tw_off[2 * j2],
+                                             tw_l + p.tw_off[2 * j2 + 1], mod2);
+            // 7. S2 at level j2, decimation 2^(J-j2)
+            if (!(dbg & 64)) {
+                lds_lowpass(B, npath, pslot, nM2, nN2, ld2, lp_l + p.lp_off[2 * j2],
+                            lp_l + p.lp_off[2 * j2 + 1], 1 << (J - j2), p.oM, p.oN, tmp, S);
+                emit(S, npath, kbase + (j2 - j1 - 1) * L + 4 * q0, 1, img, p.K, p.oM, p.oN, out,
+                     pooled);
             }
-            __syncthreads();
-            lds_lowpass(B, g, slot, nM2, nN2, ld2, lp_l + p.lp_off[2 * j2],
-                        lp_l + p.lp_off[2 * j2 + 1], 1 << (J - j2), p.oM, p.oN, tmp, S);
-            emit(S, g, kbase + (j2 - j1 - 1) * L + l2a, 1, img, p.K, p.oM, p.oN, out, pooled);
             __syncthreads();
         }
     }
@@ -458,14 +576,21 @@ bool pair_compiled(int fm, int fn) {
 #undef WST_PAIR_EQ
     return false;
 }
+// size caps of the k_order12 instantiations (largest FFT a launch may need = PM>>j1, PN>>j1)
+#define WST_CAPS(Y, A, B) Y(A, B, 12) Y(A, B, 24) Y(A, B, 48) Y(A, B, 136)
+int cap_for(int n) { return n <= 12 ? 12 : n <= 24 ? 24 : n <= 48 ? 48 : 136; }
+
 int set_lds_attributes() {
+#define WST_O12_ATTR(A, B, C)                                                                    \
+    WST_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_order12<A, B, C>),        \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));
 #define WST_PAIR_ATTR(A, B)                                                                      \
     WST_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_prep<A, B>),              \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));    \
-    WST_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_order12<A, B>),           \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));
+    WST_CAPS(WST_O12_ATTR, A, B)
     WST_FAMILY_PAIRS(WST_PAIR_ATTR)
 #undef WST_PAIR_ATTR
+#undef WST_O12_ATTR
     return WST_OK;
 }
 void launch_prep(int fm, int fn, dim3 grid, dim3 block, size_t lds, hipStream_t st,
@@ -479,17 +604,19 @@ void launch_prep(int fm, int fn, dim3 grid, dim3 block, size_t lds, hipStream_t 
     WST_FAMILY_PAIRS(WST_PAIR_PREP)
 #undef WST_PAIR_PREP
 }
-void launch_order12(int fm, int fn, dim3 grid, dim3 block, size_t lds, hipStream_t st,
-                    const DevParams& dp, int j1, int G, int nimg, long long img0,
+void launch_order12(int fm, int fn, int cap, dim3 grid, dim3 block, size_t lds, hipStream_t st,
+                    const DevParams& dp, int j1, int G, int tmpN, int nimg, long long img0,
                     const float2* xhat, float* out, int pooled) {
-#define WST_PAIR_O12(A, B)                                                                       \
-    if (fm == A && fn == B) {                                                                    \
-        hipLaunchKernelGGL((k_order12<A, B>), grid, block, lds, st, dp, j1, G, nimg, img0, xhat,  \
-                           out, pooled);                                                         \
+#define WST_O12_LAUNCH(A, B, C)                                                                  \
+    if (fm == A && fn == B && cap == C) {                                                        \
+        hipLaunchKernelGGL((k_order12<A, B, C>), grid, block, lds, st, dp, j1, G, tmpN, nimg,     \
+                           img0, xhat, out, pooled);                                             \
         return;                                                                                  \
     }
+#define WST_PAIR_O12(A, B) WST_CAPS(WST_O12_LAUNCH, A, B)
     WST_FAMILY_PAIRS(WST_PAIR_O12)
 #undef WST_PAIR_O12
+#undef WST_O12_LAUNCH
 }
 
 }  // namespace
@@ -505,6 +632,8 @@ struct wst_plan {
     float* d_psi = nullptr;
     long long* d_psi_off = nullptr;
     float* d_lp = nullptr;
+    float4* d_psi4 = nullptr;
+    long long* d_psi4_off = nullptr;
     int* d_lp_off = nullptr;
     float2* d_tw = nullptr;
     int* d_tw_off = nullptr;
@@ -513,7 +642,7 @@ struct wst_plan {
     int fam_m = 0, fam_n = 0;   // FFT size families (odd part of PM / PN), 0 = generic DFT
     int prep_threads = 256;
     size_t prep_lds = 0;
-    std::vector<int> k1_threads, k1_G;
+    std::vector<int> k1_threads, k1_G, k1_tmpN, k1_cap;
     std::vector<size_t> k1_lds;
     // internal workspace (used when the caller passes none)
     mutable std::mutex ws_mu;
@@ -533,6 +662,8 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_tw);
     (void)hipFree(p->d_tw_off);
     (void)hipFree(p->d_o2);
+    (void)hipFree(p->d_psi4);
+    (void)hipFree(p->d_psi4_off);
     if (p->ws) (void)hipFree(p->ws);
     delete p;
 }
@@ -587,11 +718,33 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
         }
     std::vector<float> lp;
     std::vector<int> lp_off(2 * static_cast<size_t>(J));
-    for (int r = 0; r < J; ++r) {
+    for (int r = 0; r < J; ++r) {  // taps stored twice so kernels index s(c+1) + n - q unwrapped
         lp_off[2 * r] = static_cast<int>(lp.size());
-        for (double v : fb.hM[r]) lp.push_back(static_cast<float>(v));
+        for (int rep = 0; rep < 2; ++rep)
+            for (double v : fb.hM[r]) lp.push_back(static_cast<float>(v));
         lp_off[2 * r + 1] = static_cast<int>(lp.size());
-        for (double v : fb.hN[r]) lp.push_back(static_cast<float>(v));
+        for (int rep = 0; rep < 2; ++rep)
+            for (double v : fb.hN[r]) lp.push_back(static_cast<float>(v));
+    }
+    // order-2 filters psi_{j2, l2} at level r < j2, four consecutive l2 interleaved per bin
+    const int nq = (L + 3) / 4;
+    std::vector<float4> psi4;
+    std::vector<long long> psi4_off(static_cast<size_t>(J) * J * nq, -1);
+    if (max_order >= 2) {
+        for (int j2 = 1; j2 < J; ++j2)
+            for (int r = 0; r < j2 && r < wst::psi_levels(j2, J); ++r)
+                for (int q = 0; q < nq; ++q) {
+                    psi4_off[(static_cast<size_t>(j2) * J + r) * nq + q] = static_cast<long long>(psi4.size());
+                    const size_t nb = static_cast<size_t>(g.PM >> r) * (g.PN >> r);
+                    for (size_t i = 0; i < nb; ++i) {
+                        float v[4] = {0.f, 0.f, 0.f, 0.f};
+                        for (int t = 0; t < 4; ++t) {
+                            const int l2 = 4 * q + t;
+                            if (l2 < L) v[t] = static_cast<float>(fb.psi[static_cast<size_t>(j2) * L + l2][r][i]);
+                        }
+                        psi4.push_back(make_float4(v[0], v[1], v[2], v[3]));
+                    }
+                }
     }
     std::vector<float2> tw;
     std::vector<int> tw_off(2 * static_cast<size_t>(J + 1));
@@ -622,6 +775,8 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     if ((rc = upload(&plan->d_tw, tw)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_tw_off, tw_off)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_o2, o2)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_psi4, psi4)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_psi4_off, psi4_off)) != WST_OK) return rc;
     plan->lp_off_h = lp_off;
     plan->tw_off_h = tw_off;
 
@@ -631,11 +786,17 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     dp.mM = g.mM; dp.mN = g.mN; dp.oM = g.oM; dp.oN = g.oN;
     dp.padTop = g.padTop; dp.padLeft = g.padLeft;
     dp.tw_total = static_cast<int>(tw.size());
+    {
+        const char* dbg = std::getenv("WST_DEBUG_SKIP");
+        dp.dbg_skip = dbg ? std::atoi(dbg) : 0;
+    }
     dp.lp_total = static_cast<int>(lp.size());
     dp.psi = plan->d_psi; dp.psi_off = plan->d_psi_off;
     dp.lp = plan->d_lp; dp.lp_off = plan->d_lp_off;
     dp.tw = plan->d_tw; dp.tw_off = plan->d_tw_off;
     dp.o2_base = plan->d_o2;
+    dp.psi4 = plan->d_psi4;
+    dp.psi4_off = plan->d_psi4_off;
 
     // --- LDS budgets ---
     const size_t tables = align16(tw.size() * sizeof(float2)) + align16(lp.size() * sizeof(float));
@@ -650,23 +811,41 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     plan->k1_threads.resize(J);
     plan->k1_G.resize(J);
     plan->k1_lds.resize(J);
+    plan->k1_tmpN.resize(J);
+    plan->k1_cap.resize(J);
     for (int j1 = 0; j1 < J; ++j1) {
         const size_t n1 = static_cast<size_t>(g.PM >> j1) * (g.PN >> j1);
         const size_t n1p = static_cast<size_t>(g.PM >> j1) * ((g.PN >> j1) | 1);
         const bool do2 = max_order >= 2 && j1 < J - 1;
         const size_t slot = do2 ? static_cast<size_t>(g.PM >> (j1 + 1)) * ((g.PN >> (j1 + 1)) | 1) : 0;
-        auto lds_for = [&](int G) {
-            return align16(n1p * sizeof(float2)) + align16(G * slot * sizeof(float2)) + tables +
-                   align16((static_cast<size_t>(G) * (g.PM >> j1) * g.oN +
-                            static_cast<size_t>(G) * g.oM * g.oN + 16) * sizeof(float));
-        };
-        int G = do2 ? std::min(L, 8) : 1;
-        while (G > 1 && lds_for(G) > static_cast<size_t>(kMaxLds)) --G;
-        if (lds_for(G) > static_cast<size_t>(kMaxLds))
+        const int G = do2 ? 4 : 1;   // B region = 4 arrays of level j1+1 (float4 filter groups)
+        // low-pass scratch: rows of the largest batch the order-2 loop forms (mirrors the kernel)
+        const int nM1 = g.PM >> j1;
+        size_t tmp_rows = static_cast<size_t>(nM1);
+        int maxnp = std::max(G, L);
+        if (do2) {
+            const int nqq = (L + 3) / 4;
+            const size_t bcap = static_cast<size_t>(G) * slot;
+            for (int j2 = j1 + 1; j2 < J; ++j2) {
+                const int nM2 = g.PM >> j2;
+                const size_t pslot = static_cast<size_t>(nM2) * ((g.PN >> j2) | 1);
+                int qpb = static_cast<int>(bcap / (4 * pslot));
+                qpb = std::max(1, std::min(qpb, nqq));
+                const int npath = std::min(4 * qpb, L);
+                tmp_rows = std::max(tmp_rows, static_cast<size_t>(npath) * nM2);
+            }
+        }
+        const size_t tmpN = tmp_rows * g.oN;
+        const size_t lds = align16(n1p * sizeof(float2)) + align16(G * slot * sizeof(float2)) +
+                           tables +
+                           align16((tmpN + static_cast<size_t>(maxnp) * g.oM * g.oN + 16) * sizeof(float));
+        if (lds > static_cast<size_t>(kMaxLds))
             return fail(WST_ERR_UNSUPPORTED, "order-1 plane at j1=" + std::to_string(j1) +
                                                  " exceeds the LDS-resident path (160 KiB per CU)");
         plan->k1_G[j1] = G;
-        plan->k1_lds[j1] = lds_for(G);
+        plan->k1_lds[j1] = lds;
+        plan->k1_tmpN[j1] = static_cast<int>(tmpN);
+        plan->k1_cap[j1] = cap_for(std::max(g.PM >> j1, g.PN >> j1));
         plan->k1_threads[j1] = n1 >= 4096 ? 512 : 256;
     }
     if ((rc = set_lds_attributes()) != WST_OK) return rc;
@@ -793,9 +972,10 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
         if ((rc = timer.end(stream, 0)) != WST_OK) return rc;
         for (int j1 = 0; j1 < g.J; ++j1) {
             if ((rc = timer.begin(stream)) != WST_OK) return rc;
-            launch_order12(plan->fam_m, plan->fam_n, dim3(nimg * g.L), dim3(plan->k1_threads[j1]),
-                           plan->k1_lds[j1], stream, plan->dp, j1, plan->k1_G[j1], nimg,
-                           static_cast<long long>(c0), xhat, d_out, pooled);
+            launch_order12(plan->fam_m, plan->fam_n, plan->k1_cap[j1], dim3(nimg * g.L),
+                           dim3(plan->k1_threads[j1]), plan->k1_lds[j1], stream, plan->dp, j1,
+                           plan->k1_G[j1], plan->k1_tmpN[j1], nimg, static_cast<long long>(c0), xhat,
+                           d_out, pooled);
             WST_HIP_CHECK(hipGetLastError());
             if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
         }
