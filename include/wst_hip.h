@@ -114,10 +114,12 @@ int wst_host_filter(int M, int N, int J, int L, int kind, int j, int l, int r, d
  * of the LDS FFTs (csrc/fft_lds.h) sequentially on `data` (complex64 interleaved), in place.
  * Line (b, l) element e lives at complex index b*bs + l*ls + e*es; n is the line length,
  * `threads` the workgroup size whose round structure is emulated; inverse is unnormalised.
- * Sizes without a compiled FFT run the generic DFT the kernels fall back to.
+ * mode 0: natural -> natural; 1: natural -> digit-reversed (in place); 2: digit-reversed ->
+ * natural (in place).  `perm` (nullable, n ints) receives the digit-reversal map (physical
+ * position -> logical index).  Sizes without a compiled FFT run the generic DFT (mode 0 only).
  */
-int wst_host_fft_lines(int n, int inverse, float* data, int nb, int bs, int nl, int ls, int es,
-                       int threads);
+int wst_host_fft_lines(int n, int inverse, int mode, float* data, int nb, int bs, int nl, int ls,
+                       int es, int threads, int* perm);
 
 #ifdef __cplusplus
 }

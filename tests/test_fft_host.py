@@ -35,7 +35,39 @@ def test_line_fft_rows_and_cols(n, inverse):
     cols = 3
     z = (rng.standard_normal((n, cols)) + 1j * rng.standard_normal((n, cols))).astype(np.complex64)
     zb = z.reshape(-1).copy()
-    _lib.host_fft_lines(zb, n, inverse, 1, 0, cols, 1, cols, 128)
+    _lib.host_fft_lines(zb, n, inverse, 1, 0, cols, 1, cols, 128, mode=0)
     ref = np.fft.ifft(z.astype(np.complex128), axis=0) * n if inverse else np.fft.fft(z.astype(np.complex128), axis=0)
     err = np.abs(zb.reshape(n, cols) - ref).max() / np.abs(ref).max()
     assert err < 3e-6 * max(1.0, np.log2(n)), (n, inverse, "cols", err)
+
+
+COMPILED = [n for n in SIZES[:26]]
+
+
+@pytest.mark.parametrize("n", COMPILED)
+@pytest.mark.parametrize("inverse", [False, True])
+def test_inplace_digit_reversed_roundtrip(n, inverse):
+    """mode 1 (natural -> digit-reversed) and mode 2 (digit-reversed -> natural), as the order-1/2
+    kernels chain them: position p of a mode-1 output holds logical bin perm[p]."""
+    rng = np.random.default_rng(100 + n)
+    rows = 4
+    ld = n | 1
+    x = (rng.standard_normal((rows, n)) + 1j * rng.standard_normal((rows, n))).astype(np.complex64)
+    buf = np.zeros(rows * ld, np.complex64)
+    for r in range(rows):
+        buf[r * ld: r * ld + n] = x[r]
+    y = buf.copy()
+    perm = _lib.host_fft_lines(y, n, inverse, 1, 0, rows, ld, 1, 256, mode=1)
+    assert sorted(perm.tolist()) == list(range(n))
+    got = np.stack([y[r * ld: r * ld + n] for r in range(rows)])
+    ref = (np.fft.ifft(x.astype(np.complex128), axis=-1) * n if inverse
+           else np.fft.fft(x.astype(np.complex128), axis=-1))
+    tol = 3e-6 * max(1.0, np.log2(n))
+    assert np.abs(got - ref[:, perm]).max() / np.abs(ref).max() < tol
+    # mode 2 on digit-reversed input returns natural order
+    z = np.zeros(rows * ld, np.complex64)
+    for r in range(rows):
+        z[r * ld: r * ld + n] = x[r][perm]
+    _lib.host_fft_lines(z, n, inverse, 1, 0, rows, ld, 1, 256, mode=2)
+    got2 = np.stack([z[r * ld: r * ld + n] for r in range(rows)])
+    assert np.abs(got2 - ref).max() / np.abs(ref).max() < tol

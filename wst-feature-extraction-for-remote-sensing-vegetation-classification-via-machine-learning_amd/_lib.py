@@ -12,8 +12,8 @@ import threading
 
 import numpy as np
 
-LIB_NAME = "libwst_hip.so"
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+LIB_NAME = os.environ.get("WST_LIB", "libwst_hip.so")   # WST_LIB: A/B-test builds in the pkg dir
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.path.basename(LIB_NAME))
 
 WST_OK, WST_ERR_INVALID, WST_ERR_UNSUPPORTED, WST_ERR_HIP, WST_ERR_NOMEM = 0, 1, 2, 3, 4
 ABI_VERSION = 1
@@ -75,7 +75,7 @@ def load() -> ctypes.CDLL:
         lib.wst_host_filter.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                         ctypes.POINTER(ctypes.c_double), c_i64]
         lib.wst_host_fft_lines.restype = c_int
-        lib.wst_host_fft_lines.argtypes = [c_int, c_int, c_vp] + [c_int] * 6
+        lib.wst_host_fft_lines.argtypes = [c_int, c_int, c_int, c_vp] + [c_int] * 6 + [c_vp]
         v = lib.wst_abi_version()
         if v != ABI_VERSION:
             raise RuntimeError(f"{LIB_NAME} ABI version {v} != expected {ABI_VERSION}; rebuild it")
@@ -100,11 +100,16 @@ def host_filter(M, N, J, L, kind, j, l, r, size) -> np.ndarray:
     return out
 
 
-def host_fft_lines(data: np.ndarray, n, inverse, nb, bs, nl, ls, es, threads=256) -> None:
-    """In-place host emulation of the device line FFT on a complex64 buffer (test hook)."""
+def host_fft_lines(data: np.ndarray, n, inverse, nb, bs, nl, ls, es, threads=256, mode=0):
+    """In-place host emulation of the device line FFT on a complex64 buffer (test hook).
+    mode 0 natural->natural, 1 natural->digit-reversed, 2 digit-reversed->natural.
+    Returns the digit-reversal map (physical position -> logical index)."""
     assert data.dtype == np.complex64 and data.flags.c_contiguous
-    check(load().wst_host_fft_lines(int(n), 1 if inverse else 0, data.ctypes.data, int(nb),
-                                    int(bs), int(nl), int(ls), int(es), int(threads)))
+    perm = np.zeros(n, np.int32)
+    check(load().wst_host_fft_lines(int(n), 1 if inverse else 0, int(mode), data.ctypes.data,
+                                    int(nb), int(bs), int(nl), int(ls), int(es), int(threads),
+                                    perm.ctypes.data))
+    return perm
 
 
 class Plan:

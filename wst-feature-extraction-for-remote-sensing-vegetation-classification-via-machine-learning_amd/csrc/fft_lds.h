@@ -295,6 +295,68 @@ struct LineFFT {
             q[e * N1 * g.es] = epi(v[e]);
         });
     }
+    // ---- in-place digit-reversed variants (no transposing store) ----
+    // F_DR = stageA_unit then stageB_inplace: natural in -> position k2 + N2*k1 holds k1 + N1*k2.
+    template <class Epi>
+    static WST_HD void stageB_inplace(float2* base, const Lines& g, int u, Epi& epi) {
+        const int nlines = g.nlines();
+        const int line = u % nlines;
+        const int k1 = u / nlines;
+        float2* p = base + g.offset(line) + (N2 * k1) * g.es;
+        float2 v[N2];
+        static_for<0, N2>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            v[e] = p[e * g.es];
+        });
+        rfft<N2, INV>(v);
+        static_for<0, N2>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            p[e * g.es] = epi(v[e]);
+        });
+    }
+    // G = stageBp_unit then stageAp_unit: digit-reversed in -> natural out.
+    static WST_HD void stageBp_unit(float2* base, const Lines& g, const float2* tw, int u) {
+        const int nlines = g.nlines();
+        const int line = u % nlines;
+        const int k1 = u / nlines;
+        float2* p = base + g.offset(line) + (N2 * k1) * g.es;
+        float2 v[N2];
+        static_for<0, N2>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            v[e] = p[e * g.es];
+        });
+        rfft<N2, INV>(v);
+        static_for<1, N2>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            v[e] = cmul_tw(v[e], tw[e * k1], INV);
+        });
+        static_for<0, N2>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            p[e * g.es] = v[e];
+        });
+    }
+    template <class Epi>
+    static WST_HD void stageAp_unit(float2* base, const Lines& g, int u, Epi& epi) {
+        const int nlines = g.nlines();
+        const int line = u % nlines;
+        const int n2 = u / nlines;
+        float2* p = base + g.offset(line) + n2 * g.es;
+        float2 v[N1];
+        static_for<0, N1>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            v[e] = p[e * N2 * g.es];
+        });
+        rfft<N1, INV>(v);
+        static_for<0, N1>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            p[e * N2 * g.es] = epi(v[e]);
+        });
+    }
+    // logical index held at physical position `pos` after F_DR (identity for single-stage sizes)
+    static constexpr WST_HD int dr_logical(int pos) {
+        return (N2 == 1) ? pos : (pos / N2) + N1 * (pos % N2);
+    }
+
     static WST_HD int lines_per_round(int T) {
         const int l = (T * UPT) / N1;
         return l < 1 ? 1 : l;
@@ -304,7 +366,7 @@ struct LineFFT {
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
 // Device driver.  Ends with a barrier.
 template <int N, bool INV, class Epi = EpiIdentity>
-__device__ void fft_lines(float2* base, const Lines g, const float2* tw, Epi& epi) {
+__device__ __forceinline__ void fft_lines(float2* base, const Lines g, const float2* tw, Epi& epi) {
     using F = LineFFT<N, INV>;
     const int T = blockDim.x;
     const int nlines = g.nlines();
@@ -336,6 +398,73 @@ __device__ void fft_lines(float2* base, const Lines g, const float2* tw, Epi& ep
     }
 }
 #endif
+
+#if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
+// timing-ablation switches for the in-place transforms (0 in production; set by the plan from
+// WST_DEBUG_FFT): 1 skip stage A, 2 skip stage B, 4 skip row passes, 8 skip column passes
+__device__ int g_dbg_fft = 0;
+
+// In-place natural -> digit-reversed transform (F_DR).  Ends with a barrier.
+template <int N, bool INV, class Epi>
+__device__ __forceinline__ void fft_lines_dr(float2* base, const Lines g, const float2* tw, Epi& epi) {
+    using F = LineFFT<N, INV>;
+    const int T = blockDim.x;
+    const int nlines = g.nlines();
+    const int dbg = g_dbg_fft;
+    if ((dbg & 4) && g.es == 1) { __syncthreads(); return; }
+    if ((dbg & 8) && g.es != 1) { __syncthreads(); return; }
+    if constexpr (F::N2 == 1) {
+        for (int u = threadIdx.x; u < nlines; u += T) F::single_unit(base, g, u, epi);
+    } else {
+        if (!(dbg & 1))
+            for (int u = threadIdx.x; u < nlines * F::N2; u += T) F::stageA_unit(base, g, tw, u);
+        __syncthreads();
+        if (!(dbg & 2))
+            for (int u = threadIdx.x; u < nlines * F::N1; u += T) F::stageB_inplace(base, g, u, epi);
+    }
+    __syncthreads();
+}
+// In-place digit-reversed -> natural transform (G).  Ends with a barrier.
+template <int N, bool INV, class Epi>
+__device__ __forceinline__ void fft_lines_rd(float2* base, const Lines g, const float2* tw, Epi& epi) {
+    using F = LineFFT<N, INV>;
+    const int T = blockDim.x;
+    const int nlines = g.nlines();
+    if constexpr (F::N2 == 1) {
+        for (int u = threadIdx.x; u < nlines; u += T) F::single_unit(base, g, u, epi);
+    } else {
+        for (int u = threadIdx.x; u < nlines * F::N1; u += T) F::stageBp_unit(base, g, tw, u);
+        __syncthreads();
+        for (int u = threadIdx.x; u < nlines * F::N2; u += T) F::stageAp_unit(base, g, u, epi);
+    }
+    __syncthreads();
+}
+#endif
+
+// Host emulation of the in-place variants: mode 1 = F_DR, mode 2 = G.
+template <int N, bool INV>
+inline void fft_lines_inplace_host(float2* base, const Lines g, const float2* tw, int mode) {
+    using F = LineFFT<N, INV>;
+    EpiIdentity epi;
+    const int nlines = g.nlines();
+    if constexpr (F::N2 == 1) {
+        for (int u = 0; u < nlines; ++u) F::single_unit(base, g, u, epi);
+    } else if (mode == 1) {
+        for (int u = 0; u < nlines * F::N2; ++u) F::stageA_unit(base, g, tw, u);
+        for (int u = 0; u < nlines * F::N1; ++u) F::stageB_inplace(base, g, u, epi);
+    } else {
+        for (int u = 0; u < nlines * F::N1; ++u) F::stageBp_unit(base, g, tw, u);
+        for (int u = 0; u < nlines * F::N2; ++u) F::stageAp_unit(base, g, u, epi);
+    }
+}
+
+// Host-side digit-reversal map (same split as the device code): logical index at `pos`.
+inline int dr_logical_host(int n, int pos) {
+    const int n2 = split_n2(n);
+    if (n2 == 1) return pos;
+    const int n1 = n / n2;
+    return pos / n2 + n1 * (pos % n2);
+}
 
 // Host emulation with the same unit bodies (sequential "threads", barriers implicit).
 template <int N, bool INV>

@@ -69,6 +69,9 @@ struct DevParams {
     const float2* tw;             // concatenated twiddle tables exp(-2 pi i k / n)
     const int* tw_off;            // [2r] -> n = PM>>r, [2r+1] -> n = PN>>r, r in [0, J]
     const int* o2_base;           // first order-2 coefficient of each n1 = j1*L + l1
+    const int* perm;              // digit-reversal maps: physical position -> logical index
+    const int* perm_off;          // [2r] -> size PM>>r, [2r+1] -> size PN>>r, r in [0, J]
+    int perm_total;
     const float4* psi4;           // order-2 filters, 4 consecutive l2 interleaved per bin
     const long long* psi4_off;    // [(j2*J + r)*ceil(L/4) + q] -> level r of l2 in [4q, 4q+4)
 };
@@ -111,7 +114,7 @@ struct EpiModulus {
 // Generic O(n) DFT along lines (fallback for sizes without a compiled FFT).  Lines are processed
 // in chunks of whole lines that fit the register tile: read phase -> barrier -> write phase.
 template <class Epi>
-__device__ void lds_dft_lines_generic(float2* base, const wstfft::Lines g, int n, const float2* tw,
+__device__ __forceinline__ void lds_dft_lines_generic(float2* base, const wstfft::Lines g, int n, const float2* tw,
                                       bool inverse, Epi& epi) {
     const int T = blockDim.x;
     const int lines_total = g.nlines();
@@ -161,25 +164,34 @@ __device__ void lds_dft_lines_generic(float2* base, const wstfft::Lines g, int n
 // n-point transforms along lines.  FAM > 0: the compiled FFTs n = FAM * 2^k <= MAXN (a plan's
 // level sizes always belong to its family, so no fallback is compiled into these kernels);
 // FAM == 0: generic DFT for any n.
-template <int FAM, int K, int MAXN, bool INV, class Epi>
+// Line-transform orders: natural -> natural (transposing store rounds), natural -> digit-reversed
+// (in place, F_DR) and digit-reversed -> natural (in place, G).
+enum { kNat = 0, kDR = 1, kRD = 2 };
+
+template <int FAM, int K, int MAXN, int KIND, bool INV, class Epi>
 __device__ __forceinline__ void family_fft(float2* base, const wstfft::Lines& g, int n,
                                            const float2* tw, Epi& epi) {
     constexpr int NN = FAM << K;
     if constexpr (NN <= MAXN && NN <= wstfft::kMaxFamilyN) {
         if constexpr (NN >= 2) {
             if (n == NN) {
-                wstfft::fft_lines<NN, INV>(base, g, tw, epi);
+                if constexpr (KIND == kNat) wstfft::fft_lines<NN, INV>(base, g, tw, epi);
+                else if constexpr (KIND == kDR) wstfft::fft_lines_dr<NN, INV>(base, g, tw, epi);
+                else wstfft::fft_lines_rd<NN, INV>(base, g, tw, epi);
                 return;
             }
         }
-        family_fft<FAM, K + 1, MAXN, INV>(base, g, n, tw, epi);
+        family_fft<FAM, K + 1, MAXN, KIND, INV>(base, g, n, tw, epi);
     }
 }
 
-template <int FAM, int MAXN, bool INV, class Epi>
-__device__ void lds_fft_lines(float2* base, const wstfft::Lines g, int n, const float2* tw, Epi& epi) {
+// n-point transforms along lines.  FAM > 0: the compiled FFTs n = FAM * 2^k <= MAXN (a plan's
+// level sizes always belong to its family, so no fallback is compiled into these kernels);
+// FAM == 0: generic DFT (natural order for every KIND; the plan's permutation maps are identity).
+template <int FAM, int MAXN, int KIND, bool INV, class Epi>
+__device__ __forceinline__ void lds_fft_lines(float2* base, const wstfft::Lines g, int n, const float2* tw, Epi& epi) {
     if constexpr (FAM > 0)
-        family_fft<FAM, 0, MAXN, INV>(base, g, n, tw, epi);
+        family_fft<FAM, 0, MAXN, KIND, INV>(base, g, n, tw, epi);
     else
         lds_dft_lines_generic(base, g, n, tw, INV, epi);
 }
@@ -187,12 +199,12 @@ __device__ void lds_fft_lines(float2* base, const wstfft::Lines g, int n, const 
 // 2-D transform of nb (rows x cols) arrays with row stride ld (odd), spaced bs apart; `epi` is
 // applied to the final (column-pass) stores.  FM / FN: size families of rows / cols; MAXN caps
 // the compiled sizes (smaller caps -> fewer registers for the small-level kernels).
-template <int FM, int FN, int MAXN, bool INV, class Epi>
-__device__ void lds_fft2(float2* buf, int nb, int bs, int rows, int cols, int ld, const float2* twR,
+template <int FM, int FN, int MAXN, int KIND, bool INV, class Epi>
+__device__ __forceinline__ void lds_fft2(float2* buf, int nb, int bs, int rows, int cols, int ld, const float2* twR,
                          const float2* twC, Epi& epi) {
     wstfft::EpiIdentity id;
-    lds_fft_lines<FN, MAXN, INV>(buf, wstfft::Lines{nb, bs, rows, ld, 1}, cols, twC, id);  // rows
-    lds_fft_lines<FM, MAXN, INV>(buf, wstfft::Lines{nb, bs, cols, 1, ld}, rows, twR, epi); // cols
+    lds_fft_lines<FN, MAXN, KIND, INV>(buf, wstfft::Lines{nb, bs, rows, ld, 1}, cols, twC, id);
+    lds_fft_lines<FM, MAXN, KIND, INV>(buf, wstfft::Lines{nb, bs, cols, 1, ld}, rows, twR, epi);
 }
 
 // Separable phi low-pass evaluated at the kept output points (unpad folded in):
@@ -200,10 +212,11 @@ __device__ void lds_fft2(float2* buf, int nb, int bs, int rows, int cols, int ld
 // hM2 / hN2 are the taps stored twice (length 2n) so s(c+1) + n - q never wraps.  U real (.x),
 // row stride ld.  tmp: nb*rows*oN floats, S: nb*oM*oN floats.  Step 1 computes OW output columns
 // per pass over a row (oN > OW: several passes).  Ends with a barrier.
+// permM / permN (nullable): logical row / column index of each physical row / column of U.
 template <int OW>
-__device__ void lds_lowpass_t(const float2* U, int nb, int bs, int rows, int cols, int ld,
-                              const float* hM2, const float* hN2, int s, int oM, int oN, float* tmp,
-                              float* S) {
+__device__ __forceinline__ void lds_lowpass_t(const float2* U, int nb, int bs, int rows, int cols, int ld,
+                              const float* hM2, const float* hN2, const int* permM,
+                              const int* permN, int s, int oM, int oN, float* tmp, float* S) {
     const int T = blockDim.x;
     const int nchunk = (oN + OW - 1) / OW;
     for (int it = threadIdx.x; it < nb * rows * nchunk; it += T) {
@@ -217,15 +230,26 @@ __device__ void lds_lowpass_t(const float2* U, int nb, int bs, int rows, int col
 #pragma unroll
         for (int c = 0; c < OW; ++c) acc[c] = 0.f;
         const float* h0 = hN2 + cols + s * (c0 + 1);   // tap index s(c+1) + cols - q
+        if (permN) {
 #pragma unroll 4
-        for (int q = 0; q < cols; ++q) {
-            const float x = row[q].x;
+            for (int q = 0; q < cols; ++q) {
+                const float x = row[q].x;
+                const float* hq = h0 - permN[q];
 #pragma unroll
-            for (int c = 0; c < OW; ++c) acc[c] = fmaf(x, h0[s * c - q], acc[c]);
+                for (int c = 0; c < OW; ++c) acc[c] = fmaf(x, hq[s * c], acc[c]);
+            }
+        } else {
+#pragma unroll 4
+            for (int q = 0; q < cols; ++q) {
+                const float x = row[q].x;
+#pragma unroll
+                for (int c = 0; c < OW; ++c) acc[c] = fmaf(x, h0[s * c - q], acc[c]);
+            }
         }
+        const int pl = permM ? permM[p] : p;            // store at the logical row
 #pragma unroll
         for (int c = 0; c < OW; ++c)
-            if (c0 + c < oN) tmp[bp * oN + c0 + c] = acc[c];
+            if (c0 + c < oN) tmp[(b * rows + pl) * oN + c0 + c] = acc[c];
     }
     __syncthreads();
     const int tot2 = nb * oM * oN;
@@ -248,18 +272,18 @@ __device__ void lds_lowpass_t(const float2* U, int nb, int bs, int rows, int col
     __syncthreads();
 }
 
-__device__ void lds_lowpass(const float2* U, int nb, int bs, int rows, int cols, int ld,
-                            const float* hM2, const float* hN2, int s, int oM, int oN, float* tmp,
-                            float* S) {
+__device__ __forceinline__ void lds_lowpass(const float2* U, int nb, int bs, int rows, int cols, int ld,
+                            const float* hM2, const float* hN2, const int* permM, const int* permN,
+                            int s, int oM, int oN, float* tmp, float* S) {
     if (oN <= 4)
-        lds_lowpass_t<4>(U, nb, bs, rows, cols, ld, hM2, hN2, s, oM, oN, tmp, S);
+        lds_lowpass_t<4>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, tmp, S);
     else
-        lds_lowpass_t<8>(U, nb, bs, rows, cols, ld, hM2, hN2, s, oM, oN, tmp, S);
+        lds_lowpass_t<8>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, tmp, S);
 }
 
 // Write nb coefficient maps (S: nb x oM x oN) of plane `img`, coefficient k0 + b*kstride.
 // pooled: out[img][k] = mean, out[img][K + k] = population std.
-__device__ void emit(const float* S, int nb, int k0, int kstride, long long img, int K, int oM,
+__device__ __forceinline__ void emit(const float* S, int nb, int k0, int kstride, long long img, int K, int oM,
                      int oN, float* out, int pooled) {
     const int npix = oM * oN;
     if (!pooled) {
@@ -288,32 +312,40 @@ __device__ void emit(const float* S, int nb, int k0, int kstride, long long img,
 }
 
 // Copy the twiddle and low-pass pools into LDS.
-__device__ void load_tables(const DevParams& p, float2* tw_l, float* lp_l) {
+__device__ __forceinline__ void load_tables(const DevParams& p, float2* tw_l, float* lp_l) {
     for (int i = threadIdx.x; i < p.tw_total; i += blockDim.x) tw_l[i] = p.tw[i];
     for (int i = threadIdx.x; i < p.lp_total; i += blockDim.x) lp_l[i] = p.lp[i];
 }
 
+// Row stride of LDS arrays: odd (conflict-free row-wise b64 access); WST_LD_EVEN for A/B tests.
+#ifdef WST_LD_EVEN
+__host__ __device__ inline int odd_ld(int n) { return n; }
+#else
 __host__ __device__ inline int odd_ld(int n) { return n | 1; }
+#endif
 
 // Order-2 fold of one group of (up to) 4 paths:
-//   B_b[u][v] = sum_{i,j < S} A[u + i nM2][v + j nN2] * psi_b[u + i nM2][v + j nN2]
+//   B_b[u][v] = sum_{i,j < s} A[u + i nM2][v + j nN2] * psi_b[u + i nM2][v + j nN2]
 // A: U1hat (stride ld1), psi4: the 4 paths' filters interleaved per bin (float4, dense nN1 rows).
+// S > 0: compile-time alias count (fully unrolled); S == 0: runtime s (large s = tiny outputs).
 template <int S>
-__device__ void fold4(const float2* A, int ld1, int nN1, const float4* __restrict__ psi4, float2* B,
-                      int slot, int ld2, int nM2, int nN2, int g) {
+__device__ __forceinline__ void fold4(const float2* A, int ld1, int nN1,
+                                      const float4* __restrict__ psi4, float2* B, int slot, int ld2,
+                                      int nM2, int nN2, int g, int s_rt) {
+    const int s = (S > 0) ? S : s_rt;
     const int items = nM2 * nN2;
     for (int it = threadIdx.x; it < items; it += blockDim.x) {
         const int u = it / nN2, v = it - (it / nN2) * nN2;
         float2 acc[4];
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc[b] = make_float2(0.f, 0.f);
-#pragma unroll(S <= 4 ? S : 1)
-        for (int i = 0; i < S; ++i) {
+#pragma unroll(S == 2 ? 2 : 1)
+        for (int i = 0; i < s; ++i) {
             const int su = u + i * nM2;
             const float2* arow = A + su * ld1 + v;
             const float4* frow = psi4 + su * nN1 + v;
-#pragma unroll(S <= 8 ? S : 8)
-            for (int j = 0; j < S; ++j) {
+#pragma unroll(S > 0 ? S : 2)
+            for (int j = 0; j < s; ++j) {
                 const float2 a = arow[j * nN2];
                 const float4 f = frow[j * nN2];
                 acc[0] = make_float2(fmaf(a.x, f.x, acc[0].x), fmaf(a.y, f.x, acc[0].y));
@@ -329,25 +361,23 @@ __device__ void fold4(const float2* A, int ld1, int nN1, const float4* __restric
     }
 }
 
-__device__ void fold4_any(int s2, const float2* A, int ld1, int nN1, const float4* psi4, float2* B,
-                          int slot, int ld2, int nM2, int nN2, int g) {
-    switch (s2) {
-        case 2: fold4<2>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g); break;
-        case 4: fold4<4>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g); break;
-        case 8: fold4<8>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g); break;
-        case 16: fold4<16>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g); break;
-        case 32: fold4<32>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g); break;
-        default: fold4<64>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g); break;
-    }
+__device__ __forceinline__ void fold4_any(int s2, const float2* A, int ld1, int nN1,
+                                          const float4* psi4, float2* B, int slot, int ld2,
+                                          int nM2, int nN2, int g) {
+    if (s2 == 2) fold4<2>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g, 2);
+    else if (s2 == 4) fold4<4>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g, 4);
+    else fold4<0>(A, ld1, nN1, psi4, B, slot, ld2, nM2, nN2, g, s2);
 }
 
-// Order-1 fold from HBM/L2: A[u][v] = sum_{i,j < S} X[u + i nM1][v + j nN1] * psi0[...]
+// Order-1 fold from HBM/L2: A[u][v] = sum_{i,j < s} X[u + i nM1][v + j nN1] * psi0[...]
+// S > 0: compile-time alias count; S == 0: runtime s.  U items per thread keep loads in flight.
 template <int S>
-__device__ void fold1(const float2* __restrict__ X, const float* __restrict__ psi0, int PN, float2* A,
-                      int ld1, int nM1, int nN1) {
+__device__ __forceinline__ void fold1(const float2* __restrict__ X, const float* __restrict__ psi0,
+                                      int PN, float2* A, int ld1, int nM1, int nN1, int s_rt) {
+    const int s = (S > 0) ? S : s_rt;
     const int items = nM1 * nN1;
     const int T = blockDim.x;
-    constexpr int U = (S == 1) ? 4 : (S == 2 ? 2 : 1);   // items per thread in flight
+    constexpr int U = (S == 1) ? 4 : (S == 2 ? 2 : 1);
     for (int it0 = threadIdx.x; it0 < items; it0 += U * T) {
         float2 acc[U];
         int dst[U];
@@ -359,10 +389,10 @@ __device__ void fold1(const float2* __restrict__ X, const float* __restrict__ ps
             if (it < items) {
                 const int u = it / nN1, v = it - (it / nN1) * nN1;
                 dst[k] = u * ld1 + v;
-#pragma unroll
-                for (int i = 0; i < S; ++i) {
-#pragma unroll
-                    for (int j = 0; j < S; ++j) {
+#pragma unroll(S > 0 ? S : 1)
+                for (int i = 0; i < s; ++i) {
+#pragma unroll(S > 0 ? S : 4)
+                    for (int j = 0; j < s; ++j) {
                         const int idx = (u + i * nM1) * PN + v + j * nN1;
                         const float f = psi0[idx];
                         const float2 xv = X[idx];
@@ -377,15 +407,12 @@ __device__ void fold1(const float2* __restrict__ X, const float* __restrict__ ps
     }
 }
 
-__device__ void fold1_any(int s1, const float2* X, const float* psi0, int PN, float2* A, int ld1,
-                          int nM1, int nN1) {
-    switch (s1) {
-        case 1: fold1<1>(X, psi0, PN, A, ld1, nM1, nN1); break;
-        case 2: fold1<2>(X, psi0, PN, A, ld1, nM1, nN1); break;
-        case 4: fold1<4>(X, psi0, PN, A, ld1, nM1, nN1); break;
-        case 8: fold1<8>(X, psi0, PN, A, ld1, nM1, nN1); break;
-        default: fold1<16>(X, psi0, PN, A, ld1, nM1, nN1); break;
-    }
+__device__ __forceinline__ void fold1_any(int s1, const float2* X, const float* psi0, int PN,
+                                          float2* A, int ld1, int nM1, int nN1) {
+    if (s1 == 1) fold1<1>(X, psi0, PN, A, ld1, nM1, nN1, 1);
+    else if (s1 == 2) fold1<2>(X, psi0, PN, A, ld1, nM1, nN1, 2);
+    else if (s1 == 4) fold1<4>(X, psi0, PN, A, ld1, nM1, nN1, 4);
+    else fold1<0>(X, psi0, PN, A, ld1, nM1, nN1, s1);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -427,8 +454,8 @@ __global__ void __launch_bounds__(512) k_prep(DevParams p, const float* __restri
     const float mean = block_sum(part, red) / n;  // contains the barrier after the gather
 
     // S0: low-pass at level 0, decimation 2^J
-    lds_lowpass(A, 1, 0, PM, PN, ld, lp_l + p.lp_off[0], lp_l + p.lp_off[1], 1 << p.J, p.oM, p.oN,
-                tmp, S);
+    lds_lowpass(A, 1, 0, PM, PN, ld, lp_l + p.lp_off[0], lp_l + p.lp_off[1], nullptr, nullptr,
+                1 << p.J, p.oM, p.oN, tmp, S);
     emit(S, 1, 0, 1, img, p.K, p.oM, p.oN, out, pooled);
 
     // mean-centred forward DFT for the band-pass paths
@@ -438,8 +465,8 @@ __global__ void __launch_bounds__(512) k_prep(DevParams p, const float* __restri
     }
     __syncthreads();
     wstfft::EpiIdentity id;
-    lds_fft2<FM, FN, wstfft::kMaxFamilyN, false>(A, 1, 0, PM, PN, ld, tw_l + p.tw_off[0],
-                                                 tw_l + p.tw_off[1], id);
+    lds_fft2<FM, FN, wstfft::kMaxFamilyN, kNat, false>(A, 1, 0, PM, PN, ld, tw_l + p.tw_off[0],
+                                                       tw_l + p.tw_off[1], id);
     float2* dst = xhat + local * n;
     for (int o = threadIdx.x; o < n; o += blockDim.x) {
         const int u = o / PN, v = o - (o / PN) * PN;
@@ -451,7 +478,7 @@ __global__ void __launch_bounds__(512) k_prep(DevParams p, const float* __restri
 // k_order12: one workgroup per (plane, theta1) at fixed j1
 // ------------------------------------------------------------------------------------------
 template <int FM, int FN, int MAXN>
-__global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int tmpN, int nimg,
+__global__ void __launch_bounds__(1024) k_order12(DevParams p, int j1, int G, int tmpN, int nimg,
                                                  long long img0, const float2* __restrict__ xhat,
                                                  float* __restrict__ out, int pooled) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -474,11 +501,13 @@ __global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int
     float2* B = A + nM1 * ld1;
     float2* tw_l = B + G * slot;
     float* lp_l = reinterpret_cast<float*>(tw_l + p.tw_total);
-    float* tmp = lp_l + p.lp_total;                   // tmpN floats (host-sized low-pass scratch)
+    int* perm_l = reinterpret_cast<int*>(lp_l + p.lp_total);
+    float* tmp = reinterpret_cast<float*>(perm_l + p.perm_total);   // tmpN floats (low-pass scratch)
     float* S = tmp + tmpN;                            // <= max(G, L) * oM * oN
     float* red = S + max(G, L) * p.oM * p.oN;         // 16
 
     load_tables(p, tw_l, lp_l);
+    for (int i = threadIdx.x; i < p.perm_total; i += blockDim.x) perm_l[i] = p.perm[i];
     const int dbg = p.dbg_skip;
 
     // 1. fold_{2^j1}(Xhat * psi0_{j1,l1}) straight from HBM/L2
@@ -490,15 +519,16 @@ __global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int
     // 2. U1 = |ifft(.)| fused into the last FFT pass; normalisation of fold-mean + ifft = 1/(PM PN)
     EpiModulus mod1{1.f / (static_cast<float>(PM) * static_cast<float>(PN)), 0.f};
     if (!(dbg & 1))
-        lds_fft2<FM, FN, MAXN, true>(A, 1, 0, nM1, nN1, ld1, tw_l + p.tw_off[2 * j1],
-                                     tw_l + p.tw_off[2 * j1 + 1], mod1);
+        lds_fft2<FM, FN, MAXN, kDR, true>(A, 1, 0, nM1, nN1, ld1, tw_l + p.tw_off[2 * j1],
+                                          tw_l + p.tw_off[2 * j1 + 1], mod1);
     const float mean1 = block_sum(mod1.sum, red) / n1;
 
     // 3. S1 at level j1, decimation 2^(J-j1)
     const int n1idx = j1 * L + l1;
     if (!(dbg & 2)) {
         lds_lowpass(A, 1, 0, nM1, nN1, ld1, lp_l + p.lp_off[2 * j1], lp_l + p.lp_off[2 * j1 + 1],
-                    1 << (J - j1), p.oM, p.oN, tmp, S);
+                    perm_l + p.perm_off[2 * j1], perm_l + p.perm_off[2 * j1 + 1], 1 << (J - j1),
+                    p.oM, p.oN, tmp, S);
         emit(S, 1, 1 + n1idx, 1, img, p.K, p.oM, p.oN, out, pooled);
     }
     if (!do2) return;
@@ -511,8 +541,8 @@ __global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int
     __syncthreads();
     wstfft::EpiIdentity id;
     if (!(dbg & 4))
-        lds_fft2<FM, FN, MAXN, false>(A, 1, 0, nM1, nN1, ld1, tw_l + p.tw_off[2 * j1],
-                                      tw_l + p.tw_off[2 * j1 + 1], id);
+        lds_fft2<FM, FN, MAXN, kRD, false>(A, 1, 0, nM1, nN1, ld1, tw_l + p.tw_off[2 * j1],
+                                           tw_l + p.tw_off[2 * j1 + 1], id);
 
     const int kbase = p.o2_base[n1idx];
     const int nq = (L + 3) >> 2;
@@ -538,12 +568,14 @@ __global__ void __launch_bounds__(512) k_order12(DevParams p, int j1, int G, int
             // 6. U2 = |ifft(.)| (modulus fused), scale 1/(nM1 nN1)
             EpiModulus mod2{1.f / static_cast<float>(n1), 0.f};
             if (!(dbg & 16))
-                lds_fft2<FM, FN, MAXN, true>(B, npath, pslot, nM2, nN2, ld2, tw_l + p.tw_off[2 * j2],
-                                             tw_l + p.tw_off[2 * j2 + 1], mod2);
+                lds_fft2<FM, FN, MAXN, kDR, true>(B, npath, pslot, nM2, nN2, ld2,
+                                                  tw_l + p.tw_off[2 * j2], tw_l + p.tw_off[2 * j2 + 1],
+                                                  mod2);
             // 7. S2 at level j2, decimation 2^(J-j2)
             if (!(dbg & 64)) {
                 lds_lowpass(B, npath, pslot, nM2, nN2, ld2, lp_l + p.lp_off[2 * j2],
-                            lp_l + p.lp_off[2 * j2 + 1], 1 << (J - j2), p.oM, p.oN, tmp, S);
+                            lp_l + p.lp_off[2 * j2 + 1], perm_l + p.perm_off[2 * j2],
+                            perm_l + p.perm_off[2 * j2 + 1], 1 << (J - j2), p.oM, p.oN, tmp, S);
                 emit(S, npath, kbase + (j2 - j1 - 1) * L + 4 * q0, 1, img, p.K, p.oM, p.oN, out,
                      pooled);
             }
@@ -638,6 +670,8 @@ struct wst_plan {
     float2* d_tw = nullptr;
     int* d_tw_off = nullptr;
     int* d_o2 = nullptr;
+    int* d_perm = nullptr;
+    int* d_perm_off = nullptr;
     // launch geometry
     int fam_m = 0, fam_n = 0;   // FFT size families (odd part of PM / PN), 0 = generic DFT
     int prep_threads = 256;
@@ -662,6 +696,8 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_tw);
     (void)hipFree(p->d_tw_off);
     (void)hipFree(p->d_o2);
+    (void)hipFree(p->d_perm);
+    (void)hipFree(p->d_perm_off);
     (void)hipFree(p->d_psi4);
     (void)hipFree(p->d_psi4_off);
     if (p->ws) (void)hipFree(p->ws);
@@ -704,6 +740,21 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     if (!plan) return fail(WST_ERR_NOMEM, "host allocation failed");
     plan->g = g;
     WST_HIP_CHECK(hipGetDevice(&plan->device));
+
+    plan->fam_m = family_of(g.PM);
+    plan->fam_n = family_of(g.PN);
+    if (!pair_compiled(plan->fam_m, plan->fam_n)) plan->fam_m = plan->fam_n = 0;
+    // digit-reversal maps of k_order12's in-place transforms (identity for the generic DFT)
+    std::vector<int> perm;
+    std::vector<int> perm_off(2 * static_cast<size_t>(J + 1));
+    for (int r = 0; r <= J; ++r)
+        for (int d = 0; d < 2; ++d) {
+            const int n = (d == 0 ? g.PM : g.PN) >> r;
+            const bool compiled = (d == 0 ? plan->fam_m : plan->fam_n) > 0;
+            perm_off[2 * r + d] = static_cast<int>(perm.size());
+            for (int pos = 0; pos < n; ++pos)
+                perm.push_back(compiled ? wstfft::dr_logical_host(n, pos) : pos);
+        }
 
     // --- flatten filters ---
     std::vector<float> psi;
@@ -777,6 +828,8 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     if ((rc = upload(&plan->d_o2, o2)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_psi4, psi4)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_psi4_off, psi4_off)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_perm, perm)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_perm_off, perm_off)) != WST_OK) return rc;
     plan->lp_off_h = lp_off;
     plan->tw_off_h = tw_off;
 
@@ -789,6 +842,9 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     {
         const char* dbg = std::getenv("WST_DEBUG_SKIP");
         dp.dbg_skip = dbg ? std::atoi(dbg) : 0;
+        const char* dfft = std::getenv("WST_DEBUG_FFT");
+        const int v = dfft ? std::atoi(dfft) : 0;
+        WST_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(wstfft::g_dbg_fft), &v, sizeof(int)));
     }
     dp.lp_total = static_cast<int>(lp.size());
     dp.psi = plan->d_psi; dp.psi_off = plan->d_psi_off;
@@ -797,11 +853,14 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     dp.o2_base = plan->d_o2;
     dp.psi4 = plan->d_psi4;
     dp.psi4_off = plan->d_psi4_off;
+    dp.perm = plan->d_perm;
+    dp.perm_off = plan->d_perm_off;
+    dp.perm_total = static_cast<int>(perm.size());
 
     // --- LDS budgets ---
     const size_t tables = align16(tw.size() * sizeof(float2)) + align16(lp.size() * sizeof(float));
     const size_t P2 = static_cast<size_t>(g.PM) * g.PN;
-    plan->prep_lds = align16(static_cast<size_t>(g.PM) * (g.PN | 1) * sizeof(float2)) + tables +
+    plan->prep_lds = align16(static_cast<size_t>(g.PM) * odd_ld(g.PN) * sizeof(float2)) + tables +
                      align16((static_cast<size_t>(g.PM) * g.oN + g.oM * g.oN + 16) * sizeof(float));
     if (plan->prep_lds > static_cast<size_t>(kMaxLds))
         return fail(WST_ERR_UNSUPPORTED,
@@ -815,9 +874,9 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     plan->k1_cap.resize(J);
     for (int j1 = 0; j1 < J; ++j1) {
         const size_t n1 = static_cast<size_t>(g.PM >> j1) * (g.PN >> j1);
-        const size_t n1p = static_cast<size_t>(g.PM >> j1) * ((g.PN >> j1) | 1);
+        const size_t n1p = static_cast<size_t>(g.PM >> j1) * odd_ld(g.PN >> j1);
         const bool do2 = max_order >= 2 && j1 < J - 1;
-        const size_t slot = do2 ? static_cast<size_t>(g.PM >> (j1 + 1)) * ((g.PN >> (j1 + 1)) | 1) : 0;
+        const size_t slot = do2 ? static_cast<size_t>(g.PM >> (j1 + 1)) * odd_ld(g.PN >> (j1 + 1)) : 0;
         const int G = do2 ? 4 : 1;   // B region = 4 arrays of level j1+1 (float4 filter groups)
         // low-pass scratch: rows of the largest batch the order-2 loop forms (mirrors the kernel)
         const int nM1 = g.PM >> j1;
@@ -828,7 +887,7 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
             const size_t bcap = static_cast<size_t>(G) * slot;
             for (int j2 = j1 + 1; j2 < J; ++j2) {
                 const int nM2 = g.PM >> j2;
-                const size_t pslot = static_cast<size_t>(nM2) * ((g.PN >> j2) | 1);
+                const size_t pslot = static_cast<size_t>(nM2) * odd_ld(g.PN >> j2);
                 int qpb = static_cast<int>(bcap / (4 * pslot));
                 qpb = std::max(1, std::min(qpb, nqq));
                 const int npath = std::min(4 * qpb, L);
@@ -837,7 +896,7 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
         }
         const size_t tmpN = tmp_rows * g.oN;
         const size_t lds = align16(n1p * sizeof(float2)) + align16(G * slot * sizeof(float2)) +
-                           tables +
+                           tables + align16(perm.size() * sizeof(int)) +
                            align16((tmpN + static_cast<size_t>(maxnp) * g.oM * g.oN + 16) * sizeof(float));
         if (lds > static_cast<size_t>(kMaxLds))
             return fail(WST_ERR_UNSUPPORTED, "order-1 plane at j1=" + std::to_string(j1) +
@@ -846,12 +905,20 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
         plan->k1_lds[j1] = lds;
         plan->k1_tmpN[j1] = static_cast<int>(tmpN);
         plan->k1_cap[j1] = cap_for(std::max(g.PM >> j1, g.PN >> j1));
-        plan->k1_threads[j1] = n1 >= 4096 ? 512 : 256;
+        // measured on MI355X (c2): 96^2 -> 1024, 48^2 -> 256, 24^2 -> 128, 12^2 -> 64 threads
+        plan->k1_threads[j1] = n1 >= 8192 ? 1024 : n1 >= 2048 ? 256 : n1 >= 512 ? 128 : 64;
+    }
+    if (const char* thr = std::getenv("WST_K1_THREADS")) {   // tuning override "t0,t1,..."
+        int j = 0;
+        for (const char* c = thr; *c && j < J; ++j) {
+            const int t = std::atoi(c);
+            if (t >= 64 && t <= 1024 && t % 64 == 0) plan->k1_threads[j] = t;
+            while (*c && *c != ',') ++c;
+            if (*c == ',') ++c;
+        }
     }
     if ((rc = set_lds_attributes()) != WST_OK) return rc;
-    plan->fam_m = family_of(g.PM);
-    plan->fam_n = family_of(g.PN);
-    if (!pair_compiled(plan->fam_m, plan->fam_n)) plan->fam_m = plan->fam_n = 0;
+
     *out = plan.release();
     g_last_error.clear();
     return WST_OK;
@@ -1042,9 +1109,10 @@ int wst_host_filter(int M, int N, int J, int L, int kind, int j, int l, int r, d
     return WST_OK;
 }
 
-int wst_host_fft_lines(int n, int inverse, float* data, int nb, int bs, int nl, int ls, int es,
-                       int threads) {
-    if (!data || n < 1 || nb < 1 || nl < 1 || threads < 1) return fail(WST_ERR_INVALID, "bad arguments");
+int wst_host_fft_lines(int n, int inverse, int mode, float* data, int nb, int bs, int nl, int ls,
+                       int es, int threads, int* perm) {
+    if (!data || n < 1 || nb < 1 || nl < 1 || threads < 1 || mode < 0 || mode > 2)
+        return fail(WST_ERR_INVALID, "bad arguments");
     std::vector<float2> tw(static_cast<size_t>(n));
     for (int k = 0; k < n; ++k) {
         const double a = 2.0 * 3.14159265358979323846 * k / n;
@@ -1052,17 +1120,28 @@ int wst_host_fft_lines(int n, int inverse, float* data, int nb, int bs, int nl, 
     }
     float2* base = reinterpret_cast<float2*>(data);
     const wstfft::Lines g{nb, bs, nl, ls, es};
+    bool compiled = false;
     switch (n) {
-#define WST_HOST_CASE(NN)                                                          \
-    case NN:                                                                       \
-        if (inverse) wstfft::fft_lines_host<NN, true>(base, g, tw.data(), threads); \
-        else wstfft::fft_lines_host<NN, false>(base, g, tw.data(), threads);        \
-        return WST_OK;
+#define WST_HOST_CASE(NN)                                                                  \
+    case NN:                                                                               \
+        compiled = true;                                                                   \
+        if (mode == 0) {                                                                   \
+            if (inverse) wstfft::fft_lines_host<NN, true>(base, g, tw.data(), threads);    \
+            else wstfft::fft_lines_host<NN, false>(base, g, tw.data(), threads);           \
+        } else {                                                                           \
+            if (inverse) wstfft::fft_lines_inplace_host<NN, true>(base, g, tw.data(), mode); \
+            else wstfft::fft_lines_inplace_host<NN, false>(base, g, tw.data(), mode);      \
+        }                                                                                  \
+        break;
         WST_FFT_SIZES(WST_HOST_CASE)
 #undef WST_HOST_CASE
         default:
             break;
     }
+    if (perm)
+        for (int pos = 0; pos < n; ++pos) perm[pos] = compiled ? wstfft::dr_logical_host(n, pos) : pos;
+    if (compiled) return WST_OK;
+    if (mode != 0) return fail(WST_ERR_UNSUPPORTED, "in-place modes need a compiled FFT size");
     // generic DFT, same arithmetic as lds_dft_lines_generic
     const float sgn = inverse ? -1.f : 1.f;
     std::vector<float2> line(static_cast<size_t>(n));
