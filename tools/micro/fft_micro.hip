@@ -17,7 +17,7 @@ struct EpiMod {
 };
 
 template <int N, int KIND, bool INV, bool MOD, int LDP, int OFFKB = 0, int TWKB = -1>
-__global__ void __launch_bounds__(512) kfft(const float2* __restrict__ in, float2* __restrict__ out,
+__global__ void __launch_bounds__(1024) kfft(const float2* __restrict__ in, float2* __restrict__ out,
                                             const float2* __restrict__ twg, int reps) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int LD = N + LDP;
@@ -78,14 +78,15 @@ int main(int argc, char** argv) {
         hipMemcpy(dtw, tw.data(), n * 8, hipMemcpyHostToDevice);
     };
     settw(96);
-    run<96, 1, true, true, 1>("DR inv +mod A@0", nblk, 512, reps, din, dout, dtw);
-    run<96, 1, true, true, 1, 80>("DR inv +mod A@80K", nblk, 512, reps, din, dout, dtw);
-    run<96, 1, true, true, 1, 0, 150>("DR inv +mod A@0 tw@150K", nblk, 512, reps, din, dout, dtw);
-    run<96, 2, false, false, 1, 0, 150>("RD fwd A@0 tw@150K", nblk, 512, reps, din, dout, dtw);
+    run<96, 1, true, true, 1>("DR+mod 512thr 2WG/CU", nblk, 512, reps, din, dout, dtw);
+    run<96, 1, true, true, 1, 80>("DR+mod 512thr 1WG/CU", nblk, 512, reps, din, dout, dtw);
+    run<96, 1, true, true, 1, 80>("DR+mod 1024thr 1WG/CU", nblk, 1024, reps, din, dout, dtw);
+    run<96, 1, true, true, 1>("DR+mod 1024thr 2WG/CU", nblk, 1024, reps, din, dout, dtw);
+    run<96, 1, true, true, 1>("DR+mod 256thr 2WG/CU", nblk, 256, reps, din, dout, dtw);
     settw(48);
-    run<48, 1, true, true, 1>("DR inv +mod A@0", nblk, 512, reps, din, dout, dtw);
-    run<48, 1, true, true, 1, 70>("DR inv +mod A@70K", nblk, 512, reps, din, dout, dtw);
-    run<48, 1, true, true, 1, 132>("DR inv +mod A@132K", nblk, 512, reps, din, dout, dtw);
+    run<48, 1, true, true, 1>("48 DR+mod 256thr ~8WG/CU", nblk, 256, reps, din, dout, dtw);
+    run<48, 1, true, true, 1, 130>("48 DR+mod 1024thr 1WG/CU", nblk, 1024, reps, din, dout, dtw);
+    run<48, 1, true, true, 1, 60>("48 DR+mod 512thr 2WG/CU", nblk, 512, reps, din, dout, dtw);
     hipDeviceSynchronize();
     return 0;
 }

@@ -105,7 +105,7 @@ struct EpiModulus {
     float scale;
     float sum;
     __device__ float2 operator()(float2 z) {
-        const float m = sqrtf(fmaf(z.x, z.x, z.y * z.y)) * scale;
+        const float m = __builtin_amdgcn_sqrtf(fmaf(z.x, z.x, z.y * z.y)) * scale;   // v_sqrt_f32
         sum += m;
         return make_float2(m, 0.f);
     }
@@ -210,75 +210,77 @@ __device__ __forceinline__ void lds_fft2(float2* buf, int nb, int bs, int rows, 
 // Separable phi low-pass evaluated at the kept output points (unpad folded in):
 //   S[b][a][c] = sum_p hM[s(a+1) - p] * sum_q hN[s(c+1) - q] * U[b][p][q]   (indices mod n)
 // hM2 / hN2 are the taps stored twice (length 2n) so s(c+1) + n - q never wraps.  U real (.x),
-// row stride ld.  tmp: nb*rows*oN floats, S: nb*oM*oN floats.  Step 1 computes OW output columns
-// per pass over a row (oN > OW: several passes).  Ends with a barrier.
-// permM / permN (nullable): logical row / column index of each physical row / column of U.
-template <int OW>
-__device__ __forceinline__ void lds_lowpass_t(const float2* U, int nb, int bs, int rows, int cols, int ld,
-                              const float* hM2, const float* hN2, const int* permM,
-                              const int* permN, int s, int oM, int oN, float* tmp, float* S) {
+// row stride ld; permM / permN (nullable): logical row / column index of each physical one.
+// Step 1: QC consecutive lanes split one row's q range and shuffle-reduce OW output columns;
+// step 2: PC consecutive lanes split the p range of one output.  tmp: nb*rows*oN floats (logical
+// rows), S: nb*oM*oN floats.  Ends with a barrier.
+template <int OW, int QC, int PC>
+__device__ __forceinline__ void lds_lowpass_t(const float2* U, int nb, int bs, int rows, int cols,
+                                              int ld, const float* hM2, const float* hN2,
+                                              const int* permM, const int* permN, int s, int oM,
+                                              int oN, float* tmp, float* S) {
     const int T = blockDim.x;
-    const int nchunk = (oN + OW - 1) / OW;
-    for (int it = threadIdx.x; it < nb * rows * nchunk; it += T) {
-        const int ch = it % nchunk;
-        const int bp = it / nchunk;
+    const int nch = (oN + OW - 1) / OW;
+    const int tot1 = nb * rows * nch * QC;
+    for (int w = threadIdx.x; w < tot1; w += T) {
+        const int qc = w & (QC - 1);
+        const int r = w / QC;
+        const int ch = r % nch;
+        const int bp = r / nch;
         const int b = bp / rows;
         const int p = bp - b * rows;
         const int c0 = ch * OW;
         const float2* row = U + b * bs + p * ld;
+        const float* h0 = hN2 + cols + s * (c0 + 1);   // tap index s(c+1) + cols - q
         float acc[OW];
 #pragma unroll
         for (int c = 0; c < OW; ++c) acc[c] = 0.f;
-        const float* h0 = hN2 + cols + s * (c0 + 1);   // tap index s(c+1) + cols - q
-        if (permN) {
-#pragma unroll 4
-            for (int q = 0; q < cols; ++q) {
-                const float x = row[q].x;
-                const float* hq = h0 - permN[q];
+#pragma unroll 2
+        for (int q = qc; q < cols; q += QC) {
+            const float x = row[q].x;
+            const float* hq = h0 - (permN ? permN[q] : q);
 #pragma unroll
-                for (int c = 0; c < OW; ++c) acc[c] = fmaf(x, hq[s * c], acc[c]);
-            }
-        } else {
-#pragma unroll 4
-            for (int q = 0; q < cols; ++q) {
-                const float x = row[q].x;
-#pragma unroll
-                for (int c = 0; c < OW; ++c) acc[c] = fmaf(x, h0[s * c - q], acc[c]);
-            }
+            for (int c = 0; c < OW; ++c) acc[c] = fmaf(x, hq[s * c], acc[c]);
         }
-        const int pl = permM ? permM[p] : p;            // store at the logical row
 #pragma unroll
-        for (int c = 0; c < OW; ++c)
-            if (c0 + c < oN) tmp[(b * rows + pl) * oN + c0 + c] = acc[c];
+        for (int off = QC / 2; off >= 1; off >>= 1)
+#pragma unroll
+            for (int c = 0; c < OW; ++c) acc[c] += __shfl_xor(acc[c], off, 64);
+        if (qc == 0) {
+            const int pl = permM ? permM[p] : p;   // store at the logical row
+#pragma unroll
+            for (int c = 0; c < OW; ++c)
+                if (c0 + c < oN) tmp[(b * rows + pl) * oN + c0 + c] = acc[c];
+        }
     }
     __syncthreads();
-    const int tot2 = nb * oM * oN;
-    for (int o = threadIdx.x; o < tot2; o += T) {
+    const int tot2 = nb * oM * oN * PC;
+    for (int w = threadIdx.x; w < tot2; w += T) {
+        const int pc = w & (PC - 1);
+        const int o = w / PC;
         const int c = o % oN;
         const int a = (o / oN) % oM;
         const int b = o / (oN * oM);
         const float* t = tmp + b * rows * oN + c;
         const float* h = hM2 + rows + s * (a + 1);
-        float acc0 = 0.f, acc1 = 0.f;
-        int p = 0;
-#pragma unroll 4
-        for (; p + 1 < rows; p += 2) {
-            acc0 = fmaf(h[-p], t[p * oN], acc0);
-            acc1 = fmaf(h[-p - 1], t[(p + 1) * oN], acc1);
-        }
-        if (p < rows) acc0 = fmaf(h[-p], t[p * oN], acc0);
-        S[o] = acc0 + acc1;
+        float acc = 0.f;
+#pragma unroll 2
+        for (int p = pc; p < rows; p += PC) acc = fmaf(h[-p], t[p * oN], acc);
+#pragma unroll
+        for (int off = PC / 2; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (pc == 0) S[o] = acc;
     }
     __syncthreads();
 }
 
-__device__ __forceinline__ void lds_lowpass(const float2* U, int nb, int bs, int rows, int cols, int ld,
-                            const float* hM2, const float* hN2, const int* permM, const int* permN,
-                            int s, int oM, int oN, float* tmp, float* S) {
+__device__ __forceinline__ void lds_lowpass(const float2* U, int nb, int bs, int rows, int cols,
+                                            int ld, const float* hM2, const float* hN2,
+                                            const int* permM, const int* permN, int s, int oM,
+                                            int oN, float* tmp, float* S) {
     if (oN <= 4)
-        lds_lowpass_t<4>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, tmp, S);
+        lds_lowpass_t<4, 8, 16>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, tmp, S);
     else
-        lds_lowpass_t<8>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, tmp, S);
+        lds_lowpass_t<8, 8, 16>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, tmp, S);
 }
 
 // Write nb coefficient maps (S: nb x oM x oN) of plane `img`, coefficient k0 + b*kstride.
@@ -534,9 +536,12 @@ __global__ void __launch_bounds__(1024) k_order12(DevParams p, int j1, int G, in
     if (!do2) return;
 
     // 4. U1hat = fft(U1 - mean) kept in LDS
-    for (int o = threadIdx.x; o < n1; o += blockDim.x) {
-        const int u = o / nN1, v = o - (o / nN1) * nN1;
+    for (int u = threadIdx.x / nN1, v = threadIdx.x % nN1, du = blockDim.x / nN1,
+             dv = blockDim.x % nN1; u < nM1;) {
         A[u * ld1 + v].x -= mean1;
+        u += du;
+        v += dv;
+        if (v >= nN1) { v -= nN1; ++u; }
     }
     __syncthreads();
     wstfft::EpiIdentity id;
