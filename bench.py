@@ -13,7 +13,8 @@ all ranks / max-over-ranks wall time.  `--gather` additionally times an RCCL all
 pooled features (reported separately, never in `value`).
 
 Extra JSON fields:
-  roofline     : dominant kernel (k_order12) algorithmic FLOP per launch / HIP-event launch time
+  roofline     : dominant kernel (largest HIP-event time of the step; k_o2 at j1=0 on c2)
+                 algorithmic FLOP per launch / HIP-event launch time
                  vs the fp32 peak (SURVEY §8(d) flop convention 5 n^2 log2 n^2 per n x n FFT);
                  traffic from committed rocprofv3 PMC passes when they match this library build.
   cpu_baseline : the float64 oracle (oracle/kymatio_ref.py, a port of kymatio 0.3.0) run the way
@@ -49,19 +50,44 @@ def fft_flops(n1, n2):
 
 
 def alg_flops_per_plane(PM, PN, J, L, max_order=2):
-    """kymatio cascade FFT FLOPs split by the kernel that performs each path."""
+    """kymatio cascade FFT FLOPs per plane (SURVEY §8(d) convention), split by the kernel that
+    performs each part: {"k_prep": X^ + S0, "k_o1_j1=j": U1 ifft + S1 (+ the row half of the U1
+    fft when order 2 follows), "k_o2_j1=j": column half of the U1 fft + every U2 ifft/fft + S2}."""
     mM, mN = PM >> J, PN >> J
-    prep = fft_flops(PM, PN) + fft_flops(mM, mN)                    # X^ and S0
-    per_j1 = []
+    out = {"k_prep": fft_flops(PM, PN) + fft_flops(mM, mN)}
     for j1 in range(J):
         n1 = (PM >> j1, PN >> j1)
-        f = L * (2 * fft_flops(*n1) + fft_flops(mM, mN))            # U1 ifft/fft + S1
-        if max_order >= 2:
+        do2 = max_order >= 2 and j1 < J - 1
+        u1 = L * fft_flops(*n1)
+        out[f"k_o1_j1={j1}"] = u1 + L * fft_flops(mM, mN) + (u1 / 2 if do2 else u1)
+        if do2:
+            f = u1 / 2
             for j2 in range(j1 + 1, J):
                 n2 = (PM >> j2, PN >> j2)
-                f += L * L * (2 * fft_flops(*n2) + fft_flops(mM, mN))   # U2 ifft/fft + S2
-        per_j1.append(f)
-    return prep, per_j1
+                f += L * L * (2 * fft_flops(*n2) + fft_flops(mM, mN))
+            out[f"k_o2_j1={j1}"] = f
+    return out
+
+
+def kernel_slots(J, max_order=2):
+    """Slot order of wst_forward_profiled: [k_prep, k_o1 j1=0..J-1, k_o2 j1=0..J-1]."""
+    return ["k_prep"] + [f"k_o1_j1={j}" for j in range(J)] + [f"k_o2_j1={j}" for j in range(J)]
+
+
+def rocprof_name(slot, PM, PN, J):
+    """Template name rocprofv3 reports for a slot's kernel (size family / size cap)."""
+    def fam(P):
+        o = P
+        while o % 2 == 0:
+            o //= 2
+        return o if o in (1, 3, 5, 9, 17) and P <= 136 else 0
+    fm, fn = fam(PM), fam(PN)
+    if slot == "k_prep":
+        return f"k_prep<{fm}, {fn}>"
+    kind, j1 = slot.split("_j1=")
+    n = max(PM, PN) >> int(j1)
+    cap = 12 if n <= 12 else 24 if n <= 24 else 48 if n <= 48 else 136
+    return f"{kind}<{fm}, {fn}, {cap}>"
 
 
 def lib_sha():
@@ -72,8 +98,8 @@ def lib_sha():
     return h.hexdigest()[:16]
 
 
-def pmc_traffic(sha):
-    """HBM bytes per k_order12 launch from committed rocprofv3 PMC passes of this exact build."""
+def pmc_traffic(sha, kernel):
+    """HBM bytes per launch of `kernel` from committed rocprofv3 PMC passes of this exact build."""
     pdir = os.path.join(ROOT, "profiles")
     if not os.path.isdir(pdir):
         return None
@@ -83,8 +109,9 @@ def pmc_traffic(sha):
                 d = json.load(open(os.path.join(pdir, name)))
             except Exception:
                 continue
-            if d.get("lib_sha") == sha and "k_order12_hbm_bytes_per_launch" in d:
-                return d["k_order12_hbm_bytes_per_launch"]
+            per = d.get("hbm_bytes_per_launch", {})
+            if d.get("lib_sha") == sha and kernel in per:
+                return per[kernel]
     return None
 
 
@@ -197,34 +224,34 @@ def main():
     value = B * world * args.steps / dt
 
     # per-kernel HIP-event durations on the launch stream (separate, untimed passes)
-    nslots = 1 + J
-    acc = [0.0] * nslots
+    slots = kernel_slots(J)
+    acc = [0.0] * len(slots)
     for _ in range(args.profile_iters):
         ms = plan.forward_profiled(x.data_ptr(), planes, out.data_ptr(), args.pooled, ws.data_ptr(),
-                                   ws_bytes, stream, nslots)
+                                   ws_bytes, stream, len(slots))
         acc = [a + b for a, b in zip(acc, ms)]
-    kms = [a / args.profile_iters for a in acc]
+    kms = dict(zip(slots, (a / args.profile_iters for a in acc)))
     nchunks = math.ceil(planes / min(planes, 2048))
-    prep_f, per_j1 = alg_flops_per_plane(plan.PM, plan.PN, J, L)
-    k12_ms = sum(kms[1:])
-    k12_launches = J * nchunks
-    k12_flop = planes * sum(per_j1)
-    achieved = k12_flop / (k12_ms * 1e-3) / 1e12
+    flops = alg_flops_per_plane(plan.PM, plan.PN, J, L)
+    kms = {k: v for k, v in kms.items() if k in flops}
+    dom = max(kms, key=kms.get)                     # dominant kernel of the step
+    dom_flop = planes * flops[dom]
+    achieved = dom_flop / (kms[dom] * 1e-3) / 1e12
     sha = lib_sha()
-    traffic = pmc_traffic(sha)
+    dname = rocprof_name(dom, plan.PM, plan.PN, J)
     roofline = {
         "bound": "mfma", "pipe": "fp32 (VALU FFT butterflies; gfx950 f32 MFMA shares the 157.3 TFLOP/s peak)",
-        "kernel": "k_order12", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-        "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
-        "traffic": traffic,
-        "launches_per_step": k12_launches,
-        "avg_launch_ms": round(k12_ms / k12_launches, 4),
-        "alg_flop_per_launch": round(k12_flop / k12_launches),
-        "kernel_ms_per_step": {"k_prep": round(kms[0], 4),
-                               **{f"k_order12_j1={j}": round(kms[1 + j], 4) for j in range(J)}},
+        "kernel": f"{dom} ({dname})", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
+        "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
+        "traffic": pmc_traffic(sha, dname),
+        "launches_per_step": nchunks,
+        "avg_launch_ms": round(kms[dom] / nchunks, 4),
+        "alg_flop_per_launch": round(dom_flop / nchunks),
+        "kernel_ms_per_step": {k: round(v, 4) for k, v in kms.items()},
+        "all_kernels_tflops": round(planes * sum(flops.values()) / (sum(kms.values()) * 1e-3) / 1e12, 4),
         "lib_sha": sha,
     }
-    patch_flop = C * (prep_f + sum(per_j1))
+    patch_flop = C * sum(flops.values())
     patch_bytes = C * M * N * 4 + (C * 2 * K * 4 if args.pooled else C * K * Mo * No * 4)
     rate_per_gpu = value / world
     step_roof = {

@@ -89,8 +89,9 @@ int wst_forward(const wst_plan* plan, const float* d_in, int64_t nbatch, float* 
 /*
  * wst_forward + per-kernel timing with HIP events recorded on `stream` around every launch
  * (synchronises the stream before returning).  kernel_ms[0] = sum of k_prep launches,
- * kernel_ms[1 + j1] = sum of the k_order12 launches at scale j1 (0 <= j1 < J); n_kernel_ms is
- * the capacity of kernel_ms (entries beyond 1 + J are left untouched).  Used by bench.py for the
+ * kernel_ms[1 + j1] = sum of the k_o1 launches at scale j1 (0 <= j1 < J), kernel_ms[1 + J + j1]
+ * = sum of the k_o2 launches at scale j1 (0 <= j1 < J - 1; slot 2J stays 0); n_kernel_ms is the
+ * capacity of kernel_ms (slots beyond it are not reported).  Used by bench.py for the
  * roofline's per-kernel durations; not meant for production calls.
  */
 int wst_forward_profiled(const wst_plan* plan, const float* d_in, int64_t nbatch, float* d_out,

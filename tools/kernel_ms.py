@@ -10,9 +10,9 @@ out = torch.empty((B, plan.K, 4, 4), device="cuda")
 wsb = plan.workspace_bytes(2048); ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 for _ in range(2): plan.forward(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st)
-acc = [0.0] * 5
+acc = [0.0] * 9
 for _ in range(5):
-    ms = plan.forward_profiled(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st, 5)
+    ms = plan.forward_profiled(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st, 9)
     acc = [a + b for a, b in zip(acc, ms)]
 acc = [a / 5 for a in acc]
-print(os.environ.get("WST_LIB", "default"), "kernel ms", [round(a, 3) for a in acc], "total", round(sum(acc), 3))
+print(os.environ.get("WST_LIB", "default"), "kernel ms prep,o1[0..3],o2[0..3]", [round(a, 3) for a in acc], "total", round(sum(acc), 3))

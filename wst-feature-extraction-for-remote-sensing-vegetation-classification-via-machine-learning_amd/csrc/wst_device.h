@@ -1,0 +1,624 @@
+// Device side of the MI355X wavelet scattering transform: LDS helpers and the three kernels.
+//
+// Replaces kymatio 0.3.0's scattering2d cascade as reached from the
+// reference at src/training/train_and_save_model.py:359-376 and src/inference/inference.py:242-257.
+//
+// Per chunk of planes (plane = one channel of one patch):
+//   k_prep  (1 WG / plane)            reflect-pad gather -> S0 (separable spatial low-pass) ->
+//                                     mean-centred forward 2-D FFT -> Xhat (workspace)
+//   k_o1    (1 WG / (plane, theta1))  fold(Xhat * psi0) -> inverse FFT, |.| fused -> S1 low-pass
+//                                     -> mean-centred real-input row FFT (two rows per complex
+//                                     row) -> Hermitian half-spectrum rows -> workspace
+//   k_o2    (1 WG / (plane, theta1))  half-spectrum column FFTs -> for every (j2 > j1, theta2):
+//                                     Hermitian fold(U1hat * psi) -> inverse FFT, |.| fused ->
+//                                     S2 low-pass
+// Each kernel stays under ~80 KiB of LDS at the headline geometry (96^2 planes), so two
+// workgroups share a CU and one's barriers overlap the other's work.
+//
+// Exact rewrites (identities of the kymatio algorithm, not approximations):
+//   * sub(Y, k) then ifft at n/k  ==  ifft at n then spatial decimation by k;
+//   * phi low-pass + subsample + ifft + unpad == a separable spatial filter evaluated only at the
+//     kept output points (phi_hat levels are outer products of 1-D masked crops);
+//   * constants are removed before the psi paths (psi_hat(0) ~ 1e-16, reflect padding preserves
+//     constants), which conditions the fp32 band-pass content;
+//   * U1 is real, so U1hat(-k) = conj(U1hat(k)): only columns 0..n/2 are formed and stored.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "fft_lds.h"
+
+namespace wstdev {
+
+constexpr int kMaxLds = 160 * 1024;
+constexpr int kMaxO = 8;  // outputs per thread per generic-DFT chunk
+
+// Kernel-side description of a plan (POD, passed by value).
+struct DevParams {
+    int M, N, PM, PN, J, L, max_order, pre_pad, K;
+    int mM, mN, oM, oN, padTop, padLeft;
+    int dbg_skip;                 // timing-ablation mask (env WST_DEBUG_SKIP; 0 in production)
+    const float* psi;             // concatenated psi Fourier levels (fp32)
+    const long long* psi_off;     // [(j*L + l)*J + r]
+    const float* lp;              // spatial low-pass taps per level, each stored twice
+    const int* lp_off;            // [2r] -> hM[r], [2r+1] -> hN[r]  (r < J); [2J] = total
+    const float2* tw;             // twiddle tables exp(-2 pi i k / n)
+    const int* tw_off;            // [2r] -> n = PM>>r, [2r+1] -> n = PN>>r (r <= J); [2J+2] = total
+    const int* perm;              // digit-reversal maps: physical position -> logical index
+    const int* perm_off;          // [2r], [2r+1] (r <= J); [2J+2] = total
+    const int* o2_base;           // first order-2 coefficient of each n1 = j1*L + l1
+    const float2* psi2;           // order-2 filters, 2 consecutive l2 interleaved per bin
+    const long long* psi2_off;    // [(j2*J + r)*ceil(L/2) + q] -> level r of l2 in {2q, 2q+1}
+};
+
+// Per-launch LDS layout (byte offsets) and the table slices copied into LDS.
+struct LdsLayout {
+    int off_b;              // second data region (k_o2: B batches)
+    int off_tw, tw0, ntw;   // twiddles: global elements [tw0, tw0+ntw)
+    int off_lp, lp0, nlp;   // low-pass taps
+    int off_pm, pm0, npm;   // permutations
+    int off_s, off_red;     // S (coefficients) and reduction scratch
+    int bcap;               // complex capacity of B (k_o2)
+};
+
+// ------------------------------------------------------------------------------------------
+// helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int reflect_index(int i, int n) {
+    // numpy.pad(mode='reflect') for any pad width: even periodic extension, period 2(n-1)
+    if (n == 1) return 0;
+    const int period = 2 * (n - 1);
+    int t = i % period;
+    if (t < 0) t += period;
+    return t < n ? t : period - t;
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    float s = 0.f;
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int w = 0; w < nw; ++w) s += red[w];
+    return s;
+}
+
+// |z| * scale stored as a real value (.y = 0); accumulates the per-thread sum (for means)
+struct EpiModulus {
+    float scale;
+    float sum;
+    __device__ float2 operator()(float2 z) {
+        const float m = __builtin_amdgcn_sqrtf(fmaf(z.x, z.x, z.y * z.y)) * scale;   // v_sqrt_f32
+        sum += m;
+        return make_float2(m, 0.f);
+    }
+};
+
+// Row-major iteration of an (rows x cols) grid with stride blockDim.x, division-free.
+struct GridIter {
+    int u, v, du, dv, cols;
+    __device__ __forceinline__ GridIter(int cols_) : cols(cols_) {
+        u = threadIdx.x / cols;
+        v = threadIdx.x - u * cols;
+        du = blockDim.x / cols;
+        dv = blockDim.x - du * cols;
+    }
+    __device__ __forceinline__ void next() {
+        u += du;
+        v += dv;
+        if (v >= cols) {
+            v -= cols;
+            ++u;
+        }
+    }
+};
+
+// Generic O(n) DFT along lines (fallback family 0).  Lines are processed in chunks of whole lines
+// that fit the register tile: read phase -> barrier -> write phase.  Ends with a barrier.
+template <class Epi>
+__device__ __forceinline__ void lds_dft_lines_generic(float2* base, const wstfft::Lines g, int n,
+                                                      const float2* tw, bool inverse, Epi& epi) {
+    const int T = blockDim.x;
+    const int lines_total = g.nlines();
+    int lpc = (T * kMaxO) / n;
+    if (lpc < 1) lpc = 1;
+    const float sgn = inverse ? -1.f : 1.f;
+    for (int l0 = 0; l0 < lines_total; l0 += lpc) {
+        const int nlc = min(lpc, lines_total - l0);
+        const int nout = nlc * n;
+        float2 acc[kMaxO];
+        int addr[kMaxO];
+#pragma unroll
+        for (int i = 0; i < kMaxO; ++i) {
+            const int o = threadIdx.x + i * T;
+            addr[i] = -1;
+            acc[i] = make_float2(0.f, 0.f);
+            if (o < nout) {
+                const int lc = o / n;
+                const int k = o - lc * n;
+                const int off = g.offset(l0 + lc);
+                const float2* src = base + off;
+                float sr = 0.f, si = 0.f;
+                int idx = 0;
+                for (int e = 0; e < n; ++e) {
+                    const float2 x = src[e * g.es];
+                    const float2 w = tw[idx];
+                    const float wy = sgn * w.y;
+                    sr = fmaf(x.x, w.x, fmaf(-x.y, wy, sr));
+                    si = fmaf(x.x, wy, fmaf(x.y, w.x, si));
+                    idx += k;
+                    if (idx >= n) idx -= n;
+                }
+                acc[i] = make_float2(sr, si);
+                addr[i] = off + k * g.es;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < kMaxO; ++i)
+            if (addr[i] >= 0) base[addr[i]] = epi(acc[i]);
+    }
+    __syncthreads();
+}
+
+// Line-transform orders: natural -> natural (transposing store rounds), natural -> digit-reversed
+// (in place, F_DR) and digit-reversed -> natural (in place, G).
+enum { kNat = 0, kDR = 1, kRD = 2 };
+
+template <int FAM, int K, int MAXN, int KIND, bool INV, class Epi>
+__device__ __forceinline__ void family_fft(float2* base, const wstfft::Lines& g, int n,
+                                           const float2* tw, Epi& epi) {
+    constexpr int NN = FAM << K;
+    if constexpr (NN <= MAXN && NN <= wstfft::kMaxFamilyN) {
+        if constexpr (NN >= 2) {
+            if (n == NN) {
+                if constexpr (KIND == kNat) wstfft::fft_lines<NN, INV>(base, g, tw, epi);
+                else if constexpr (KIND == kDR) wstfft::fft_lines_dr<NN, INV>(base, g, tw, epi);
+                else wstfft::fft_lines_rd<NN, INV>(base, g, tw, epi);
+                return;
+            }
+        }
+        family_fft<FAM, K + 1, MAXN, KIND, INV>(base, g, n, tw, epi);
+    }
+}
+
+// n-point transforms along lines.  FAM > 0: the compiled FFTs n = FAM * 2^k <= MAXN (a plan's
+// level sizes always belong to its family); FAM == 0: generic DFT (natural order for every KIND;
+// the plan's permutation maps are then identity).
+template <int FAM, int MAXN, int KIND, bool INV, class Epi>
+__device__ __forceinline__ void lds_fft_lines(float2* base, const wstfft::Lines g, int n,
+                                              const float2* tw, Epi& epi) {
+    if constexpr (FAM > 0)
+        family_fft<FAM, 0, MAXN, KIND, INV>(base, g, n, tw, epi);
+    else
+        lds_dft_lines_generic(base, g, n, tw, INV, epi);
+}
+
+// 2-D transform of nb (rows x cols) arrays with row stride ld (odd), spaced bs apart; `epi` is
+// applied to the final (column-pass) stores.
+template <int FM, int FN, int MAXN, int KIND, bool INV, class Epi>
+__device__ __forceinline__ void lds_fft2(float2* buf, int nb, int bs, int rows, int cols, int ld,
+                                         const float2* twR, const float2* twC, Epi& epi) {
+    wstfft::EpiIdentity id;
+    lds_fft_lines<FN, MAXN, KIND, INV>(buf, wstfft::Lines{nb, bs, rows, ld, 1}, cols, twC, id);
+    lds_fft_lines<FM, MAXN, KIND, INV>(buf, wstfft::Lines{nb, bs, cols, 1, ld}, rows, twR, epi);
+}
+
+// Separable phi low-pass at the kept output points (unpad folded in):
+//   S[b][a][c] = sum_p hM[s(a+1) - p] * sum_q hN[s(c+1) - q] * U[b][p][q]   (indices mod n)
+// hM2 / hN2: taps stored twice so s(c+1) + n - q never wraps.  U real in .x, row stride ld;
+// permM / permN (nullable): logical index of each physical row / column.  The row partial sums
+// T[b][p][c] are parked in the .y slots of row p (the .y of a real array is free), so no scratch.
+// Step 1: QC lanes split a row and shuffle-reduce OW columns; step 2: PC lanes split the rows.
+template <int OW, int QC, int PC>
+__device__ __forceinline__ void lds_lowpass_t(float2* U, int nb, int bs, int rows, int cols, int ld,
+                                              const float* hM2, const float* hN2,
+                                              const int* permM, const int* permN, int s, int oM,
+                                              int oN, float* S) {
+    const int T = blockDim.x;
+    const int nch = (oN + OW - 1) / OW;
+    const int tot1 = nb * rows * nch * QC;
+    for (int w = threadIdx.x; w < tot1; w += T) {
+        const int qc = w & (QC - 1);
+        const int r = w / QC;
+        const int ch = r % nch;
+        const int bp = r / nch;
+        const int b = bp / rows;
+        const int p = bp - b * rows;
+        const int c0 = ch * OW;
+        float2* row = U + b * bs + p * ld;
+        const float* h0 = hN2 + cols + s * (c0 + 1);
+        float acc[OW];
+#pragma unroll
+        for (int c = 0; c < OW; ++c) acc[c] = 0.f;
+#pragma unroll 2
+        for (int q = qc; q < cols; q += QC) {
+            const float x = row[q].x;
+            const float* hq = h0 - (permN ? permN[q] : q);
+#pragma unroll
+            for (int c = 0; c < OW; ++c) acc[c] = fmaf(x, hq[s * c], acc[c]);
+        }
+#pragma unroll
+        for (int off = QC / 2; off >= 1; off >>= 1)
+#pragma unroll
+            for (int c = 0; c < OW; ++c) acc[c] += __shfl_xor(acc[c], off, 64);
+        if (qc == 0) {
+#pragma unroll
+            for (int c = 0; c < OW; ++c)
+                if (c0 + c < oN) row[c0 + c].y = acc[c];
+        }
+    }
+    __syncthreads();
+    const int tot2 = nb * oM * oN * PC;
+    for (int w = threadIdx.x; w < tot2; w += T) {
+        const int pc = w & (PC - 1);
+        const int o = w / PC;
+        const int c = o % oN;
+        const int a = (o / oN) % oM;
+        const int b = o / (oN * oM);
+        const float2* t = U + b * bs + c;
+        const float* h = hM2 + rows + s * (a + 1);
+        float acc = 0.f;
+#pragma unroll 2
+        for (int p = pc; p < rows; p += PC) acc = fmaf(h[-(permM ? permM[p] : p)], t[p * ld].y, acc);
+#pragma unroll
+        for (int off = PC / 2; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (pc == 0) S[o] = acc;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void lds_lowpass(float2* U, int nb, int bs, int rows, int cols, int ld,
+                                            const float* hM2, const float* hN2, const int* permM,
+                                            const int* permN, int s, int oM, int oN, float* S) {
+    if (oN <= 4)
+        lds_lowpass_t<4, 8, 16>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, S);
+    else
+        lds_lowpass_t<8, 8, 16>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, S);
+}
+
+// Write nb coefficient maps (S: nb x oM x oN) of plane `img`, coefficient k0 + b.
+// pooled: out[img][k] = mean, out[img][K + k] = population std.
+__device__ __forceinline__ void emit(const float* S, int nb, int k0, long long img, int K, int oM,
+                                     int oN, float* out, int pooled) {
+    const int npix = oM * oN;
+    if (!pooled) {
+        const int tot = nb * npix;
+        for (int o = threadIdx.x; o < tot; o += blockDim.x) {
+            const int b = o / npix;
+            out[(img * K + k0 + b) * npix + (o - b * npix)] = S[o];
+        }
+    } else {
+        for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+            const float* v = S + b * npix;
+            float m = 0.f;
+            for (int i = 0; i < npix; ++i) m += v[i];
+            m /= npix;
+            float q = 0.f;
+            for (int i = 0; i < npix; ++i) {
+                const float d = v[i] - m;
+                q = fmaf(d, d, q);
+            }
+            out[img * 2 * K + k0 + b] = m;
+            out[img * 2 * K + K + k0 + b] = sqrtf(q / npix);
+        }
+    }
+}
+
+// Table slices of the plan pools copied into LDS; accessors rebase global offsets.
+struct Tables {
+    float2* tw;
+    float* lp;
+    int* pm;
+    int tw0, lp0, pm0;
+    const DevParams* p;
+    __device__ __forceinline__ const float2* twM(int r) const { return tw + (p->tw_off[2 * r] - tw0); }
+    __device__ __forceinline__ const float2* twN(int r) const { return tw + (p->tw_off[2 * r + 1] - tw0); }
+    __device__ __forceinline__ const float* lpM(int r) const { return lp + (p->lp_off[2 * r] - lp0); }
+    __device__ __forceinline__ const float* lpN(int r) const { return lp + (p->lp_off[2 * r + 1] - lp0); }
+    __device__ __forceinline__ const int* pmM(int r) const { return pm + (p->perm_off[2 * r] - pm0); }
+    __device__ __forceinline__ const int* pmN(int r) const { return pm + (p->perm_off[2 * r + 1] - pm0); }
+};
+
+__device__ __forceinline__ Tables load_tables(const DevParams& p, const LdsLayout& lay,
+                                              unsigned char* smem) {
+    Tables t;
+    t.tw = reinterpret_cast<float2*>(smem + lay.off_tw);
+    t.lp = reinterpret_cast<float*>(smem + lay.off_lp);
+    t.pm = reinterpret_cast<int*>(smem + lay.off_pm);
+    t.tw0 = lay.tw0;
+    t.lp0 = lay.lp0;
+    t.pm0 = lay.pm0;
+    t.p = &p;
+    for (int i = threadIdx.x; i < lay.ntw; i += blockDim.x) t.tw[i] = p.tw[lay.tw0 + i];
+    for (int i = threadIdx.x; i < lay.nlp; i += blockDim.x) t.lp[i] = p.lp[lay.lp0 + i];
+    for (int i = threadIdx.x; i < lay.npm; i += blockDim.x) t.pm[i] = p.perm[lay.pm0 + i];
+    return t;
+}
+
+__host__ __device__ inline int odd_ld(int n) { return n | 1; }
+
+// Order-1 fold from HBM/L2: A[u][v] = sum_{i,j < s} X[u + i nM1][v + j nN1] * psi0[...]
+// S > 0: compile-time alias count; S == 0: runtime s.  U items per thread keep loads in flight.
+template <int S>
+__device__ __forceinline__ void fold1(const float2* __restrict__ X, const float* __restrict__ psi0,
+                                      int PN, float2* A, int ld1, int nM1, int nN1, int s_rt) {
+    const int s = (S > 0) ? S : s_rt;
+    const int items = nM1 * nN1;
+    const int T = blockDim.x;
+    constexpr int U = (S == 1) ? 4 : (S == 2 ? 2 : 1);
+    constexpr int UI = S > 0 ? S : 1, UJ = S > 0 ? S : 4;
+    for (int it0 = threadIdx.x; it0 < items; it0 += U * T) {
+        float2 acc[U];
+        int dst[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k) {
+            const int it = it0 + k * T;
+            acc[k] = make_float2(0.f, 0.f);
+            dst[k] = -1;
+            if (it < items) {
+                const int u = it / nN1, v = it - (it / nN1) * nN1;
+                dst[k] = u * ld1 + v;
+#pragma unroll UI
+                for (int i = 0; i < s; ++i) {
+#pragma unroll UJ
+                    for (int j = 0; j < s; ++j) {
+                        const int idx = (u + i * nM1) * PN + v + j * nN1;
+                        const float f = psi0[idx];
+                        const float2 xv = X[idx];
+                        acc[k] = make_float2(fmaf(xv.x, f, acc[k].x), fmaf(xv.y, f, acc[k].y));
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            if (dst[k] >= 0) A[dst[k]] = acc[k];
+    }
+}
+
+__device__ __forceinline__ void fold1_any(int s1, const float2* X, const float* psi0, int PN,
+                                          float2* A, int ld1, int nM1, int nN1) {
+    if (s1 == 1) fold1<1>(X, psi0, PN, A, ld1, nM1, nN1, 1);
+    else if (s1 == 2) fold1<2>(X, psi0, PN, A, ld1, nM1, nN1, 2);
+    else if (s1 == 4) fold1<4>(X, psi0, PN, A, ld1, nM1, nN1, 4);
+    else fold1<0>(X, psi0, PN, A, ld1, nM1, nN1, s1);
+}
+
+// Order-2 Hermitian fold of npair filter pairs (2 paths each) into B:
+//   B_b[u][v] = sum_{i,j < s} U1hat[u + i nM2][v + j nN2] * psi_b[...]
+// U1hat is read from the half spectrum H (nM1 x hld, columns 0..nN1/2):
+//   U1hat[kr][kc] = kc <= nN1/2 ? H[kr][kc] : conj(H[(nM1 - kr) % nM1][nN1 - kc]).
+template <int S>
+__device__ __forceinline__ void fold2(const float2* H, int hld, int nM1, int nN1,
+                                      const float2* __restrict__ psi2, long long pstride,
+                                      int npair, int npath, float2* B, int pslot, int ld2, int nM2,
+                                      int nN2, int s_rt) {
+    const int s = (S > 0) ? S : s_rt;
+    const int half = nN1 >> 1;
+    const int items = nM2 * nN2;
+    const int total = npair * items;
+    constexpr int UI = S == 2 ? 2 : 1, UJ = S > 0 ? S : 2;
+    for (int w = threadIdx.x; w < total; w += blockDim.x) {
+        const int pr = w / items;
+        const int it = w - pr * items;
+        const int u = it / nN2, v = it - (it / nN2) * nN2;
+        const float2* ps = psi2 + pr * pstride;
+        float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+#pragma unroll UI
+        for (int i = 0; i < s; ++i) {
+            const int kr = u + i * nM2;
+            const int krm = kr == 0 ? 0 : nM1 - kr;
+            const float2* frow = ps + kr * nN1;
+#pragma unroll UJ
+            for (int j = 0; j < s; ++j) {
+                const int kc = v + j * nN2;
+                const bool mir = kc > half;
+                float2 a = H[mir ? krm * hld + (nN1 - kc) : kr * hld + kc];
+                a.y = mir ? -a.y : a.y;
+                const float2 f = frow[kc];
+                a0 = make_float2(fmaf(a.x, f.x, a0.x), fmaf(a.y, f.x, a0.y));
+                a1 = make_float2(fmaf(a.x, f.y, a1.x), fmaf(a.y, f.y, a1.y));
+            }
+        }
+        float2* dst = B + 2 * pr * pslot + u * ld2 + v;
+        dst[0] = a0;
+        if (2 * pr + 1 < npath) dst[pslot] = a1;
+    }
+}
+
+__device__ __forceinline__ void fold2_any(int s2, const float2* H, int hld, int nM1, int nN1,
+                                          const float2* psi2, long long pstride, int npair,
+                                          int npath, float2* B, int pslot, int ld2, int nM2,
+                                          int nN2) {
+    if (s2 == 2) fold2<2>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, 2);
+    else if (s2 == 4) fold2<4>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, 4);
+    else fold2<0>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, s2);
+}
+
+// XCD-aware decode of (plane, theta1) items: blocks b and b+8 share an XCD; give each XCD a
+// contiguous range so the L workgroups of a plane read its Xhat from one L2.
+__device__ __forceinline__ int xcd_item(int total) {
+    int item = blockIdx.x;
+    if ((total & 7) == 0) item = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
+    return item;
+}
+
+// ------------------------------------------------------------------------------------------
+// k_prep: one workgroup per plane
+// ------------------------------------------------------------------------------------------
+template <int FM, int FN>
+__global__ void __launch_bounds__(1024) k_prep(DevParams p, LdsLayout lay,
+                                               const float* __restrict__ in, long long img0,
+                                               float2* __restrict__ xhat, float* __restrict__ out,
+                                               int pooled) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int PM = p.PM, PN = p.PN, n = PM * PN, ld = odd_ld(PN);
+    float2* A = reinterpret_cast<float2*>(smem);
+    float* S = reinterpret_cast<float*>(smem + lay.off_s);
+    float* red = reinterpret_cast<float*>(smem + lay.off_red);
+    const Tables tb = load_tables(p, lay, smem);
+
+    const long long local = blockIdx.x;
+    const long long img = img0 + local;
+    const int inM = p.pre_pad ? PM : p.M, inN = p.pre_pad ? PN : p.N;
+    const float* x = in + local * inM * inN;
+    float part = 0.f;
+    for (GridIter it(PN); it.u < PM; it.next()) {
+        const int su = p.pre_pad ? it.u : reflect_index(it.u - p.padTop, p.M);
+        const int sv = p.pre_pad ? it.v : reflect_index(it.v - p.padLeft, p.N);
+        const float val = x[su * inN + sv];
+        A[it.u * ld + it.v] = make_float2(val, 0.f);
+        part += val;
+    }
+    const float mean = block_sum(part, red) / n;  // contains the barrier after the gather
+
+    // S0: low-pass at level 0, decimation 2^J
+    lds_lowpass(A, 1, 0, PM, PN, ld, tb.lpM(0), tb.lpN(0), nullptr, nullptr, 1 << p.J, p.oM, p.oN, S);
+    emit(S, 1, 0, img, p.K, p.oM, p.oN, out, pooled);
+
+    // mean-centred forward DFT for the band-pass paths (.y reset: the low-pass parked sums there)
+    for (GridIter it(PN); it.u < PM; it.next()) {
+        float2& a = A[it.u * ld + it.v];
+        a = make_float2(a.x - mean, 0.f);
+    }
+    __syncthreads();
+    wstfft::EpiIdentity id;
+    lds_fft2<FM, FN, wstfft::kMaxFamilyN, kNat, false>(A, 1, 0, PM, PN, ld, tb.twM(0), tb.twN(0), id);
+    float2* dst = xhat + local * n;
+    for (GridIter it(PN); it.u < PM; it.next()) dst[it.u * PN + it.v] = A[it.u * ld + it.v];
+}
+
+// ------------------------------------------------------------------------------------------
+// k_o1: one workgroup per (plane, theta1) at fixed j1 -- order 1 + half-spectrum export
+// ------------------------------------------------------------------------------------------
+template <int FM, int FN, int MAXN>
+__global__ void __launch_bounds__(1024) k_o1(DevParams p, LdsLayout lay, int j1, int nimg,
+                                             long long img0, const float2* __restrict__ xhat,
+                                             float2* __restrict__ hexp, float* __restrict__ out,
+                                             int pooled) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int J = p.J, L = p.L;
+    const int item = xcd_item(nimg * L);
+    const int local = item / L;
+    const int l1 = item - local * L;
+    const long long img = img0 + local;
+    const int PM = p.PM, PN = p.PN;
+    const int nM1 = PM >> j1, nN1 = PN >> j1, n1 = nM1 * nN1, ld1 = odd_ld(nN1);
+    const bool do2 = (p.max_order >= 2) && (j1 < J - 1);
+    float2* A = reinterpret_cast<float2*>(smem);
+    float* S = reinterpret_cast<float*>(smem + lay.off_s);
+    float* red = reinterpret_cast<float*>(smem + lay.off_red);
+    const Tables tb = load_tables(p, lay, smem);
+    const int dbg = p.dbg_skip;
+
+    // 1. fold_{2^j1}(Xhat * psi0_{j1,l1}) straight from HBM/L2
+    const float* psi0 = p.psi + p.psi_off[(j1 * L + l1) * J + 0];
+    const float2* X = xhat + static_cast<long long>(local) * PM * PN;
+    if (!(dbg & 128)) fold1_any(1 << j1, X, psi0, PN, A, ld1, nM1, nN1);
+    __syncthreads();
+
+    // 2. U1 = |ifft(.)|, modulus fused into the last pass; fold-mean + ifft scale = 1/(PM PN).
+    //    In place (digit-reversed rows and columns); the low-pass maps the permutation.
+    EpiModulus mod1{1.f / (static_cast<float>(PM) * static_cast<float>(PN)), 0.f};
+    if (!(dbg & 1))
+        lds_fft2<FM, FN, MAXN, kDR, true>(A, 1, 0, nM1, nN1, ld1, tb.twM(j1), tb.twN(j1), mod1);
+    const float mean1 = block_sum(mod1.sum, red) / n1;
+
+    // 3. S1 at level j1, decimation 2^(J-j1)
+    const int n1idx = j1 * L + l1;
+    if (!(dbg & 2)) {
+        lds_lowpass(A, 1, 0, nM1, nN1, ld1, tb.lpM(j1), tb.lpN(j1), tb.pmM(j1), tb.pmN(j1),
+                    1 << (J - j1), p.oM, p.oN, S);
+        emit(S, 1, 1 + n1idx, img, p.K, p.oM, p.oN, out, pooled);
+    }
+    if (!do2) return;
+
+    // 4. real-input row FFT of (U1 - mean): physical rows 2r, 2r+1 packed as re/im of row 2r
+    const int nh = nM1 >> 1;
+    for (GridIter it(nN1); it.u < nh; it.next()) {
+        float2* a = A + (2 * it.u) * ld1 + it.v;
+        *a = make_float2(a->x - mean1, a[ld1].x - mean1);
+    }
+    __syncthreads();
+    wstfft::EpiIdentity id;
+    if (!(dbg & 4))
+        lds_fft_lines<FN, MAXN, kRD, false>(A, wstfft::Lines{1, 0, nh, 2 * ld1, 1}, nN1,
+                                            tb.twN(j1), id);
+
+    // 5. split into the two rows' half spectra (columns 0..nN1/2) and export them
+    const int hld = (nN1 >> 1) + 1;
+    float2* H = hexp + static_cast<long long>(item) * nM1 * hld;
+    for (GridIter it(hld); it.u < nh; it.next()) {
+        const float2* row = A + (2 * it.u) * ld1;
+        const float2 z = row[it.v];
+        const float2 zm = row[it.v == 0 ? 0 : nN1 - it.v];
+        H[(2 * it.u) * hld + it.v] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+        H[(2 * it.u + 1) * hld + it.v] = make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_o2: one workgroup per (plane, theta1) at fixed j1 -- all order-2 paths from U1hat
+// ------------------------------------------------------------------------------------------
+template <int FM, int FN, int MAXN>
+__global__ void __launch_bounds__(1024) k_o2(DevParams p, LdsLayout lay, int j1, int nimg,
+                                             long long img0, const float2* __restrict__ hexp,
+                                             float* __restrict__ out, int pooled) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int J = p.J, L = p.L;
+    const int item = xcd_item(nimg * L);
+    const int local = item / L;
+    const int l1 = item - local * L;
+    const long long img = img0 + local;
+    const int PM = p.PM, PN = p.PN;
+    const int nM1 = PM >> j1, nN1 = PN >> j1, n1 = nM1 * nN1;
+    const int hld = (nN1 >> 1) + 1;
+    float2* H = reinterpret_cast<float2*>(smem);
+    float2* B = reinterpret_cast<float2*>(smem + lay.off_b);
+    float* S = reinterpret_cast<float*>(smem + lay.off_s);
+    const Tables tb = load_tables(p, lay, smem);
+    const int dbg = p.dbg_skip;
+
+    // 1. half spectrum rows -> LDS, then the column FFTs (rows digit-reversed -> natural)
+    const float2* Hg = hexp + static_cast<long long>(item) * nM1 * hld;
+    for (int o = threadIdx.x; o < nM1 * hld; o += blockDim.x) H[o] = Hg[o];
+    __syncthreads();
+    wstfft::EpiIdentity id;
+    if (!(dbg & 4))
+        lds_fft_lines<FM, MAXN, kRD, false>(H, wstfft::Lines{1, 0, hld, 1, hld}, nM1, tb.twM(j1), id);
+
+    // 2. order-2 paths in batches: Hermitian fold -> |ifft| -> S2 low-pass
+    const int kbase = p.o2_base[j1 * L + l1];
+    const int nq = (L + 1) >> 1;
+    for (int j2 = j1 + 1; j2 < J; ++j2) {
+        const int nM2 = PM >> j2, nN2 = PN >> j2, ld2 = odd_ld(nN2);
+        const int pslot = nM2 * ld2;
+        const int s2 = 1 << (j2 - j1);
+        int pb = lay.bcap / pslot;                 // paths per batch (multiple of 2)
+        pb = max(2, min(pb & ~1, 2 * nq));
+        for (int l2a = 0; l2a < L; l2a += pb) {
+            const int npath = min(pb, L - l2a);
+            const int npair = (npath + 1) >> 1;
+            const float2* ps = p.psi2 + p.psi2_off[(j2 * J + j1) * nq + (l2a >> 1)];
+            const long long pstride = static_cast<long long>(n1);
+            if (!(dbg & 8))
+                fold2_any(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
+            __syncthreads();
+            EpiModulus mod2{1.f / static_cast<float>(n1), 0.f};
+            if (!(dbg & 16))
+                lds_fft2<FM, FN, MAXN, kDR, true>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
+                                                  tb.twN(j2), mod2);
+            if (!(dbg & 64)) {
+                lds_lowpass(B, npath, pslot, nM2, nN2, ld2, tb.lpM(j2), tb.lpN(j2), tb.pmM(j2),
+                            tb.pmN(j2), 1 << (J - j2), p.oM, p.oN, S);
+                emit(S, npath, kbase + (j2 - j1 - 1) * L + l2a, img, p.K, p.oM, p.oN, out, pooled);
+            }
+            __syncthreads();
+        }
+    }
+}
+
+}  // namespace wstdev
