@@ -1,8 +1,8 @@
-"""Timing ablation of k_order12 phases (dev tool): per WST_DEBUG_SKIP mask, per-kernel ms."""
+"""Timing ablation of k_o1 / k_o2 phases (dev tool): per WST_DEBUG_SKIP mask, per-kernel ms."""
 import os, subprocess, sys, json
 masks = {"full": 0, "no_o1_fold": 128, "no_o1_ifft": 1, "no_S1": 2, "no_U1_fft": 4, "no_o2_fold": 8,
-         "no_o2_ifft": 16, "no_o2_mod": 32, "no_o2_lowpass": 64, "no_order2_all": 8 | 16 | 32 | 64,
-         "only_o2_ifft": 1 | 2 | 4 | 8 | 32 | 64 | 128}
+         "no_o2_ifft": 16, "no_o2_lowpass": 64, "no_order2_paths": 8 | 16 | 64,
+         "o2_only_load": 4 | 8 | 16 | 64}
 child = r'''
 import os, sys, json
 sys.path.insert(0, os.getcwd())

@@ -1,18 +1,29 @@
-"""Per-kernel HIP-event milliseconds of one c2 forward (dev tool)."""
-import os, sys, json
+"""Per-kernel HIP-event milliseconds of one c2 forward at several chunk sizes (dev tool).
+usage: python tools/kernel_ms.py [chunk_planes ...]   (default 2048)"""
+import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import numpy as np, torch, wst_amd
+import numpy as np, torch, wst_amd  # noqa: F401
 from wst_amd import _lib
-B = 3072
+B, J = 3072, 4
 x = torch.from_numpy(np.random.default_rng(1).integers(0, 256, (B, 64, 64), dtype=np.uint8).astype(np.float32) / 255).cuda()
-plan = _lib.Plan(64, 64, 4, 8)
+plan = _lib.Plan(64, 64, J, 8)
 out = torch.empty((B, plan.K, 4, 4), device="cuda")
-wsb = plan.workspace_bytes(2048); ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
-for _ in range(2): plan.forward(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st)
-acc = [0.0] * 9
-for _ in range(5):
-    ms = plan.forward_profiled(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st, 9)
-    acc = [a + b for a, b in zip(acc, ms)]
-acc = [a / 5 for a in acc]
-print(os.environ.get("WST_LIB", "default"), "kernel ms prep,o1[0..3],o2[0..3]", [round(a, 3) for a in acc], "total", round(sum(acc), 3))
+nslot = 1 + 2 * J
+for chunk in [int(a) for a in sys.argv[1:]] or [2048]:
+    wsb = plan.workspace_bytes(chunk); ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+    for _ in range(2): plan.forward(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10): plan.forward(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st)
+    e1.record(); torch.cuda.synchronize()
+    wall = e0.elapsed_time(e1) / 10
+    acc = [0.0] * nslot
+    for _ in range(5):
+        ms = plan.forward_profiled(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st, nslot)
+        acc = [a + b for a, b in zip(acc, ms)]
+    acc = [round(a / 5, 3) for a in acc]
+    print(os.environ.get("WST_LIB", "default"), f"chunk={chunk} wall={wall:.3f} ms",
+          "prep", acc[0], "o1", acc[1:1 + J], "o2", acc[1 + J:], "sum", round(sum(acc), 3), flush=True)
+    del ws

@@ -13,7 +13,7 @@ from . import _lib
 _plan_cache: dict = {}
 _plan_lock = threading.Lock()
 
-# cap on the Xhat workspace (planes per chunk); 2048 x 96^2 x 8 B = 151 MB, MALL-resident
+# planes per workspace chunk: Xhat + the order-1 half spectra, 471 KB/plane at c2 (965 MB)
 WORKSPACE_PLANES = 2048
 
 
