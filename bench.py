@@ -98,6 +98,22 @@ def lib_sha():
     return h.hexdigest()[:16]
 
 
+def src_sha():
+    """Hash of the kernel sources + build recipe (stable across rebuilds of the same code, unlike
+    the .so bytes): ties committed PMC profiles to the code they measured."""
+    from wst_amd import _lib
+    csrc = os.path.join(os.path.dirname(_lib.LIB_PATH), "csrc")
+    h = hashlib.sha256()
+    files = sorted(os.path.join(csrc, f) for f in os.listdir(csrc)
+                   if f.endswith((".hip", ".h", ".cpp")) or f == "Makefile")
+    files.append(os.path.join(ROOT, "include", "wst_hip.h"))
+    for p in files:
+        h.update(os.path.basename(p).encode())
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(sha, kernel):
     """HBM bytes per launch of `kernel` from committed rocprofv3 PMC passes of this exact build."""
     pdir = os.path.join(ROOT, "profiles")
@@ -110,7 +126,7 @@ def pmc_traffic(sha, kernel):
             except Exception:
                 continue
             per = d.get("hbm_bytes_per_launch", {})
-            if d.get("lib_sha") == sha and kernel in per:
+            if sha in (d.get("lib_sha"), d.get("src_sha")) and kernel in per:
                 return per[kernel]
     return None
 
@@ -237,19 +253,19 @@ def main():
     dom = max(kms, key=kms.get)                     # dominant kernel of the step
     dom_flop = planes * flops[dom]
     achieved = dom_flop / (kms[dom] * 1e-3) / 1e12
-    sha = lib_sha()
+    sha = src_sha()
     dname = rocprof_name(dom, plan.PM, plan.PN, J)
     roofline = {
         "bound": "mfma", "pipe": "fp32 (VALU FFT butterflies; gfx950 f32 MFMA shares the 157.3 TFLOP/s peak)",
         "kernel": f"{dom} ({dname})", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
-        "traffic": pmc_traffic(sha, dname),
+        "traffic": pmc_traffic(sha, dname) or pmc_traffic(lib_sha(), dname),
         "launches_per_step": nchunks,
         "avg_launch_ms": round(kms[dom] / nchunks, 4),
         "alg_flop_per_launch": round(dom_flop / nchunks),
         "kernel_ms_per_step": {k: round(v, 4) for k, v in kms.items()},
         "all_kernels_tflops": round(planes * sum(flops.values()) / (sum(kms.values()) * 1e-3) / 1e12, 4),
-        "lib_sha": sha,
+        "src_sha": sha, "lib_sha": lib_sha(),
     }
     patch_flop = C * sum(flops.values())
     patch_bytes = C * M * N * 4 + (C * 2 * K * 4 if args.pooled else C * K * Mo * No * 4)

@@ -1,6 +1,6 @@
 """HBM bytes per launch per kernel from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE),
 corrected as MI355X_MICROARCH.md prescribes (FETCH_SIZE x2 on gfx950; WRITE_SIZE as is; both in
-KB units of 1024 B).  usage: python tools/pmc_hbm.py <fetch_dir> <write_dir> <lib_sha> <out.json>"""
+KB units of 1024 B).  usage: python tools/pmc_hbm.py <fetch_dir> <write_dir> <src_sha> <out.json>"""
 import collections, csv, glob, json, os, re, sys
 
 
@@ -18,7 +18,7 @@ def per_kernel(d, counter):
 
 fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
 write = per_kernel(sys.argv[2], "WRITE_SIZE")
-res = {"lib_sha": sys.argv[3], "unit": "bytes per launch (mean over dispatches)",
+res = {"src_sha": sys.argv[3], "unit": "bytes per launch (mean over dispatches)",
        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
                  "FETCH_SIZE doubled (gfx950 half-count), KB = 1024 B",
        "hbm_bytes_per_launch": {}, "fetch_bytes_per_launch": {}, "write_bytes_per_launch": {},

@@ -4,9 +4,9 @@
 tag=$1
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 99
 o=gpurun_out
-sha=$(python3 -c "import bench; print(bench.lib_sha())")
+sha=$(python3 -c "import bench; print(bench.src_sha())")
 tools/gpu_step.sh 400 $o/${tag}_bench.log python3 bench.py &&
-tools/gpu_step.sh 300 $o/${tag}_ktrace.log rocprofv3 --kernel-trace --stats -d $o/${tag}_ktrace -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
+tools/gpu_step.sh 300 $o/${tag}_ktrace.log rocprofv3 --kernel-trace --stats --output-format csv -d $o/${tag}_ktrace -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline &&
 tools/gpu_step.sh 300 $o/${tag}_fetch.log rocprofv3 --pmc FETCH_SIZE --output-format csv -d $o/${tag}_fetch -o pmc -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --profile-iters 1 &&
 tools/gpu_step.sh 300 $o/${tag}_write.log rocprofv3 --pmc WRITE_SIZE --output-format csv -d $o/${tag}_write -o pmc -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --profile-iters 1 &&
 python3 tools/pmc_hbm.py $o/${tag}_fetch $o/${tag}_write "$sha" $o/${tag}_pmc.json > /dev/null &&
