@@ -215,13 +215,45 @@ WST_HD float2 cmul_tw(float2 a, float2 w, bool conj) {
     return make_float2(fmaf(a.x, w.x, -a.y * wy), fmaf(a.x, wy, a.y * w.x));
 }
 
+// Exact division by a runtime divisor d (1 <= d < 2^20) for 0 <= x < 2^31 as one mul-hi, one add
+// and one shift (round-up magic number, as in PyTorch's IntDivider); replaces the ~20-instruction
+// integer division the compiler emits for a runtime divisor in the per-unit index decode.
+struct FastDiv {
+    unsigned m = 1;
+    int sh = 0;
+    WST_HD FastDiv() {}
+    WST_HD explicit FastDiv(int d) {
+        sh = 0;
+        while ((1 << sh) < d) ++sh;
+        // floor(2^32 (2^sh - d) / d) + 1; the double quotient is exact to the floor for d < 2^20
+        m = static_cast<unsigned>(4294967296.0 * static_cast<double>((1 << sh) - d) /
+                                  static_cast<double>(d)) + 1u;
+    }
+    WST_HD int div(int x) const {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const unsigned t = __umulhi(static_cast<unsigned>(x), m);
+#else
+        const unsigned t = static_cast<unsigned>((static_cast<unsigned long long>(x) * m) >> 32);
+#endif
+        return static_cast<int>((t + static_cast<unsigned>(x)) >> sh);
+    }
+};
+
 // Geometry of a batch of lines: line (b, l) element e at base[b*bs + l*ls + e*es].
 struct Lines {
     int nb, bs, nl, ls, es;
+    FastDiv dnl, dlines;  // / nl and / (nb * nl)
+    WST_HD Lines(int nb_, int bs_, int nl_, int ls_, int es_)
+        : nb(nb_), bs(bs_), nl(nl_), ls(ls_), es(es_), dnl(nl_), dlines(nb_ * nl_) {}
     WST_HD int nlines() const { return nb * nl; }
     WST_HD int offset(int line) const {
-        const int b = line / nl;
+        const int b = dnl.div(line);
         return b * bs + (line - b * nl) * ls;
+    }
+    // unit u of a per-line stage -> (line = u % nlines, k = u / nlines)
+    WST_HD int split(int u, int& k) const {
+        k = dlines.div(u);
+        return u - k * nb * nl;
     }
 };
 
@@ -253,9 +285,8 @@ struct LineFFT {
     }
     // stage A: unit u -> (line = u % nlines, n2 = u / nlines)
     static WST_HD void stageA_unit(float2* base, const Lines& g, const float2* tw, int u) {
-        const int nlines = g.nlines();
-        const int line = u % nlines;
-        const int n2 = u / nlines;
+        int n2;
+        const int line = g.split(u, n2);
         float2* p = base + g.offset(line) + n2 * g.es;
         float2 v[N1];
         static_for<0, N1>([&](auto ec) {
@@ -275,8 +306,8 @@ struct LineFFT {
     // stage B load+compute: round lines [L0, L0+nlr), unit w -> (line = L0 + w % nlr, k1 = w / nlr)
     static WST_HD int stageB_load(const float2* base, const Lines& g, int L0, int nlr, int w,
                                   float2 (&v)[N2]) {
-        const int line = L0 + w % nlr;
         const int k1 = w / nlr;
+        const int line = L0 + (w - k1 * nlr);
         const int lb = g.offset(line);
         const float2* p = base + lb + (N2 * k1) * g.es;
         static_for<0, N2>([&](auto ec) {
@@ -299,9 +330,8 @@ struct LineFFT {
     // F_DR = stageA_unit then stageB_inplace: natural in -> position k2 + N2*k1 holds k1 + N1*k2.
     template <class Epi>
     static WST_HD void stageB_inplace(float2* base, const Lines& g, int u, Epi& epi) {
-        const int nlines = g.nlines();
-        const int line = u % nlines;
-        const int k1 = u / nlines;
+        int k1;
+        const int line = g.split(u, k1);
         float2* p = base + g.offset(line) + (N2 * k1) * g.es;
         float2 v[N2];
         static_for<0, N2>([&](auto ec) {
@@ -316,9 +346,8 @@ struct LineFFT {
     }
     // G = stageBp_unit then stageAp_unit: digit-reversed in -> natural out.
     static WST_HD void stageBp_unit(float2* base, const Lines& g, const float2* tw, int u) {
-        const int nlines = g.nlines();
-        const int line = u % nlines;
-        const int k1 = u / nlines;
+        int k1;
+        const int line = g.split(u, k1);
         float2* p = base + g.offset(line) + (N2 * k1) * g.es;
         float2 v[N2];
         static_for<0, N2>([&](auto ec) {
@@ -337,9 +366,8 @@ struct LineFFT {
     }
     template <class Epi>
     static WST_HD void stageAp_unit(float2* base, const Lines& g, int u, Epi& epi) {
-        const int nlines = g.nlines();
-        const int line = u % nlines;
-        const int n2 = u / nlines;
+        int n2;
+        const int line = g.split(u, n2);
         float2* p = base + g.offset(line) + n2 * g.es;
         float2 v[N1];
         static_for<0, N1>([&](auto ec) {
@@ -400,27 +428,18 @@ __device__ __forceinline__ void fft_lines(float2* base, const Lines g, const flo
 #endif
 
 #if defined(__HIP_DEVICE_COMPILE__) || defined(__HIPCC__)
-// timing-ablation switches for the in-place transforms (0 in production; set by the plan from
-// WST_DEBUG_FFT): 1 skip stage A, 2 skip stage B, 4 skip row passes, 8 skip column passes
-__device__ int g_dbg_fft = 0;
-
 // In-place natural -> digit-reversed transform (F_DR).  Ends with a barrier.
 template <int N, bool INV, class Epi>
 __device__ __forceinline__ void fft_lines_dr(float2* base, const Lines g, const float2* tw, Epi& epi) {
     using F = LineFFT<N, INV>;
     const int T = blockDim.x;
     const int nlines = g.nlines();
-    const int dbg = g_dbg_fft;
-    if ((dbg & 4) && g.es == 1) { __syncthreads(); return; }
-    if ((dbg & 8) && g.es != 1) { __syncthreads(); return; }
     if constexpr (F::N2 == 1) {
         for (int u = threadIdx.x; u < nlines; u += T) F::single_unit(base, g, u, epi);
     } else {
-        if (!(dbg & 1))
-            for (int u = threadIdx.x; u < nlines * F::N2; u += T) F::stageA_unit(base, g, tw, u);
+        for (int u = threadIdx.x; u < nlines * F::N2; u += T) F::stageA_unit(base, g, tw, u);
         __syncthreads();
-        if (!(dbg & 2))
-            for (int u = threadIdx.x; u < nlines * F::N1; u += T) F::stageB_inplace(base, g, u, epi);
+        for (int u = threadIdx.x; u < nlines * F::N1; u += T) F::stageB_inplace(base, g, u, epi);
     }
     __syncthreads();
 }

@@ -49,14 +49,24 @@ struct DevParams {
     const int* o2_base;           // first order-2 coefficient of each n1 = j1*L + l1
     const float2* psi2;           // order-2 filters, 2 consecutive l2 interleaved per bin
     const long long* psi2_off;    // [(j2*J + r)*ceil(L/2) + q] -> level r of l2 in {2q, 2q+1}
+    const int* box;               // order-2 alias boxes: per pair, nM2 row then nN2 column
+                                  // entries (first alias | count << 8); pairs of one (j2, r)
+                                  // contiguous, stride box_stride[j2]
+    const int* box_off;           // [j2*J + r] -> first pair's entries
+    const float* lpt;             // low-pass tap matrices in physical (digit-reversed) order:
+    const int* lpt_off;           // [2r] GM_r (PM>>r rows x kLpOM), [2r+1] GN_r (PN>>r x oN)
 };
 
 // Per-launch LDS layout (byte offsets) and the table slices copied into LDS.
 struct LdsLayout {
     int off_b;              // second data region (k_o2: B batches)
-    int off_tw, tw0, ntw;   // twiddles: global elements [tw0, tw0+ntw)
+    int off_tw, tw0, ntw;   // twiddles: M block [tw0, tw0+ntw) then N block [twn0, twn0+ntwn)
+    int twn0, ntwn;         //   (ntwn == 0: square kernel, N tables == M tables)
     int off_lp, lp0, nlp;   // low-pass taps
     int off_pm, pm0, npm;   // permutations
+    int off_lt, lt0, nlt;   // low-pass tap matrices (lpt pool): GM block, then GN block
+    int ltn0, nltn;         //   (nltn == 0: square kernel, GN == GM)
+    int oms;                // row stride of the tap matrices (4 or kLpOM)
     int off_s, off_red;     // S (coefficients) and reduction scratch
     int bcap;               // complex capacity of B (k_o2)
 };
@@ -167,12 +177,12 @@ __device__ __forceinline__ void lds_dft_lines_generic(float2* base, const wstfft
 // (in place, F_DR) and digit-reversed -> natural (in place, G).
 enum { kNat = 0, kDR = 1, kRD = 2 };
 
-template <int FAM, int K, int MAXN, int KIND, bool INV, class Epi>
+template <int FAM, int K, int LO, int HI, int KIND, bool INV, class Epi>
 __device__ __forceinline__ void family_fft(float2* base, const wstfft::Lines& g, int n,
                                            const float2* tw, Epi& epi) {
     constexpr int NN = FAM << K;
-    if constexpr (NN <= MAXN && NN <= wstfft::kMaxFamilyN) {
-        if constexpr (NN >= 2) {
+    if constexpr (NN <= HI && NN <= wstfft::kMaxFamilyN) {
+        if constexpr (NN >= 2 && NN > LO) {
             if (n == NN) {
                 if constexpr (KIND == kNat) wstfft::fft_lines<NN, INV>(base, g, tw, epi);
                 else if constexpr (KIND == kDR) wstfft::fft_lines_dr<NN, INV>(base, g, tw, epi);
@@ -180,30 +190,31 @@ __device__ __forceinline__ void family_fft(float2* base, const wstfft::Lines& g,
                 return;
             }
         }
-        family_fft<FAM, K + 1, MAXN, KIND, INV>(base, g, n, tw, epi);
+        family_fft<FAM, K + 1, LO, HI, KIND, INV>(base, g, n, tw, epi);
     }
 }
 
-// n-point transforms along lines.  FAM > 0: the compiled FFTs n = FAM * 2^k <= MAXN (a plan's
-// level sizes always belong to its family); FAM == 0: generic DFT (natural order for every KIND;
-// the plan's permutation maps are then identity).
-template <int FAM, int MAXN, int KIND, bool INV, class Epi>
+// n-point transforms along lines.  FAM > 0: the compiled FFTs n = FAM * 2^k in (LO, HI] (a plan's
+// level sizes always belong to its family; the bounds keep a kernel's code to the sizes its
+// launches can meet); FAM == 0: generic DFT (natural order for every KIND; the plan's
+// permutation maps are then identity).
+template <int FAM, int LO, int HI, int KIND, bool INV, class Epi>
 __device__ __forceinline__ void lds_fft_lines(float2* base, const wstfft::Lines g, int n,
                                               const float2* tw, Epi& epi) {
     if constexpr (FAM > 0)
-        family_fft<FAM, 0, MAXN, KIND, INV>(base, g, n, tw, epi);
+        family_fft<FAM, 0, LO, HI, KIND, INV>(base, g, n, tw, epi);
     else
         lds_dft_lines_generic(base, g, n, tw, INV, epi);
 }
 
 // 2-D transform of nb (rows x cols) arrays with row stride ld (odd), spaced bs apart; `epi` is
 // applied to the final (column-pass) stores.
-template <int FM, int FN, int MAXN, int KIND, bool INV, class Epi>
+template <int FM, int FN, int LO, int HI, int KIND, bool INV, class Epi>
 __device__ __forceinline__ void lds_fft2(float2* buf, int nb, int bs, int rows, int cols, int ld,
                                          const float2* twR, const float2* twC, Epi& epi) {
     wstfft::EpiIdentity id;
-    lds_fft_lines<FN, MAXN, KIND, INV>(buf, wstfft::Lines{nb, bs, rows, ld, 1}, cols, twC, id);
-    lds_fft_lines<FM, MAXN, KIND, INV>(buf, wstfft::Lines{nb, bs, cols, 1, ld}, rows, twR, epi);
+    lds_fft_lines<FN, LO, HI, KIND, INV>(buf, wstfft::Lines{nb, bs, rows, ld, 1}, cols, twC, id);
+    lds_fft_lines<FM, LO, HI, KIND, INV>(buf, wstfft::Lines{nb, bs, cols, 1, ld}, rows, twR, epi);
 }
 
 // Separable phi low-pass at the kept output points (unpad folded in):
@@ -279,6 +290,122 @@ __device__ __forceinline__ void lds_lowpass(float2* U, int nb, int bs, int rows,
         lds_lowpass_t<8, 8, 16>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, S);
 }
 
+constexpr int kLpOM = 8;  // row stride of the GM tap matrices = largest oM of the fused path
+
+// Inverse column pass (in place, natural -> digit-reversed rows) of nb (NN x cols) arrays U_b,
+// fused with |.| * scale and the phi low-pass (unpad and decimation folded
+// into the tap matrices GM (physical row p -> kept output row a) and GN (column q -> output c)):
+//   1. after the last butterfly the unit holding physical rows [RU k, RU k + RU) of column q
+//      stores V_k[a] = sum_p GM[p][a] |z_p| scale (a < oM; GM rows oms = 4 or 8 floats) in its own
+//      first slots: row RU k + a/2,
+//      component a & 1 (the modulus itself is never stored);
+//   2. W[a][q] = sum_k V_k[a][q], written over V_0;
+//   3. S[b][a][c] = sum_q GN[q][c] W[a][q]  (QC lanes per output, shuffle-reduced).
+// Requires oM <= min(kLpOM, 2 RU) (host: fused_lowpass_ok).  Ends with a barrier.
+template <int NN>
+__device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, int ld,
+                                           const float2* tw, const float* GM, const float* GN,
+                                           int oms, int oM, int oN, float scale, float* S) {
+    using F = wstfft::LineFFT<NN, true>;
+    constexpr bool single = (F::N2 == 1);
+    constexpr int RU = single ? NN : F::N2;  // rows per unit
+    constexpr int NU = single ? 1 : F::N1;   // units per column
+    const wstfft::Lines g(nb, bs, cols, 1, ld);
+    const int T = blockDim.x;
+    const int nlines = nb * cols;
+    if constexpr (!single) {
+        for (int u = threadIdx.x; u < nlines * F::N2; u += T) F::stageA_unit(U, g, tw, u);
+        __syncthreads();
+    }
+    for (int u = threadIdx.x; u < nlines * NU; u += T) {
+        int k = 0;
+        const int line = single ? u : g.split(u, k);
+        float2* p = U + g.offset(line) + (RU * k) * ld;
+        float2 v[RU];
+        wstfft::static_for<0, RU>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            v[e] = p[e * ld];
+        });
+        wstfft::rfft<RU, true>(v);
+        const float* gm = GM + (RU * k) * oms;
+        float V[kLpOM];
+#pragma unroll
+        for (int a = 0; a < kLpOM; ++a) V[a] = 0.f;
+        wstfft::static_for<0, RU>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            const float m = __builtin_amdgcn_sqrtf(fmaf(v[e].x, v[e].x, v[e].y * v[e].y)) * scale;
+            const float4 g0 = *reinterpret_cast<const float4*>(gm + e * oms);
+            V[0] = fmaf(g0.x, m, V[0]);
+            V[1] = fmaf(g0.y, m, V[1]);
+            V[2] = fmaf(g0.z, m, V[2]);
+            V[3] = fmaf(g0.w, m, V[3]);
+            if (oM > 4) {
+                const float4 g1 = *reinterpret_cast<const float4*>(gm + e * oms + 4);
+                V[4] = fmaf(g1.x, m, V[4]);
+                V[5] = fmaf(g1.y, m, V[5]);
+                V[6] = fmaf(g1.z, m, V[6]);
+                V[7] = fmaf(g1.w, m, V[7]);
+            }
+        });
+#pragma unroll
+        for (int t = 0; t < kLpOM / 2; ++t)
+            if (2 * t < oM) p[t * ld] = make_float2(V[2 * t], V[2 * t + 1]);
+    }
+    __syncthreads();
+    // 2. W over the units of each column (thread = (a, line), lanes along consecutive columns)
+    if constexpr (NU > 1) {
+        const wstfft::FastDiv dl(nlines);
+        for (int w = threadIdx.x; w < nlines * oM; w += T) {
+            const int a = dl.div(w);
+            const int line = w - a * nlines;
+            float* f = reinterpret_cast<float*>(U + g.offset(line) + (a >> 1) * ld) + (a & 1);
+            float acc = 0.f;
+            wstfft::static_for<0, NU>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                acc += f[2 * RU * k * ld];
+            });
+            *f = acc;
+        }
+        __syncthreads();
+    }
+    // 3. S = W GN
+    constexpr int QC = 8;
+    const int nout = nb * oM * oN;
+    const wstfft::FastDiv dc(oN), dab(oM * oN);
+    for (int w = threadIdx.x; w < nout * QC; w += T) {
+        const int qc = w & (QC - 1);
+        const int o = w / QC;
+        const int b = dab.div(o);
+        const int ac = o - b * oM * oN;
+        const int a = dc.div(ac);
+        const int c = ac - a * oN;
+        const float* f = reinterpret_cast<const float*>(U + b * bs + (a >> 1) * ld) + (a & 1);
+        float acc = 0.f;
+        for (int q = qc; q < cols; q += QC) acc = fmaf(GN[q * oms + c], f[2 * q], acc);
+#pragma unroll
+        for (int off = QC / 2; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (qc == 0) S[o] = acc;
+    }
+    __syncthreads();
+}
+
+template <int FAM, int K, int HI>
+__device__ __forceinline__ void family_cols_modlp(float2* U, int nb, int bs, int rows, int cols,
+                                                  int ld, const float2* tw, const float* GM,
+                                                  const float* GN, int oms, int oM, int oN,
+                                                  float scale, float* S) {
+    constexpr int NN = FAM << K;
+    if constexpr (FAM > 0 && NN <= HI && NN <= wstfft::kMaxFamilyN) {
+        if constexpr (NN >= 2) {
+            if (rows == NN) {
+                cols_modlp<NN>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S);
+                return;
+            }
+        }
+        family_cols_modlp<FAM, K + 1, HI>(U, nb, bs, rows, cols, ld, tw, GM, GN, oms, oM, oN, scale, S);
+    }
+}
+
 // Write nb coefficient maps (S: nb x oM x oN) of plane `img`, coefficient k0 + b.
 // pooled: out[img][k] = mean, out[img][K + k] = population std.
 __device__ __forceinline__ void emit(const float* S, int nb, int k0, long long img, int K, int oM,
@@ -286,8 +413,9 @@ __device__ __forceinline__ void emit(const float* S, int nb, int k0, long long i
     const int npix = oM * oN;
     if (!pooled) {
         const int tot = nb * npix;
+        const wstfft::FastDiv dpix(npix);
         for (int o = threadIdx.x; o < tot; o += blockDim.x) {
-            const int b = o / npix;
+            const int b = dpix.div(o);
             out[(img * K + k0 + b) * npix + (o - b * npix)] = S[o];
         }
     } else {
@@ -312,14 +440,21 @@ struct Tables {
     float2* tw;
     float* lp;
     int* pm;
-    int tw0, lp0, pm0;
+    float* lt;
+    int tw0, lp0, pm0, lt0, ntw, twn0, ntwn, nlt, ltn0, nltn;
     const DevParams* p;
     __device__ __forceinline__ const float2* twM(int r) const { return tw + (p->tw_off[2 * r] - tw0); }
-    __device__ __forceinline__ const float2* twN(int r) const { return tw + (p->tw_off[2 * r + 1] - tw0); }
+    __device__ __forceinline__ const float2* twN(int r) const {
+        return ntwn ? tw + ntw + (p->tw_off[2 * r + 1] - twn0) : twM(r);
+    }
     __device__ __forceinline__ const float* lpM(int r) const { return lp + (p->lp_off[2 * r] - lp0); }
     __device__ __forceinline__ const float* lpN(int r) const { return lp + (p->lp_off[2 * r + 1] - lp0); }
     __device__ __forceinline__ const int* pmM(int r) const { return pm + (p->perm_off[2 * r] - pm0); }
     __device__ __forceinline__ const int* pmN(int r) const { return pm + (p->perm_off[2 * r + 1] - pm0); }
+    __device__ __forceinline__ const float* gM(int r) const { return lt + (p->lpt_off[2 * r] - lt0); }
+    __device__ __forceinline__ const float* gN(int r) const {
+        return nltn ? lt + nlt + (p->lpt_off[2 * r + 1] - ltn0) : gM(r);
+    }
 };
 
 __device__ __forceinline__ Tables load_tables(const DevParams& p, const LdsLayout& lay,
@@ -328,13 +463,24 @@ __device__ __forceinline__ Tables load_tables(const DevParams& p, const LdsLayou
     t.tw = reinterpret_cast<float2*>(smem + lay.off_tw);
     t.lp = reinterpret_cast<float*>(smem + lay.off_lp);
     t.pm = reinterpret_cast<int*>(smem + lay.off_pm);
+    t.lt = reinterpret_cast<float*>(smem + lay.off_lt);
     t.tw0 = lay.tw0;
     t.lp0 = lay.lp0;
     t.pm0 = lay.pm0;
+    t.lt0 = lay.lt0;
+    t.ntw = lay.ntw;
+    t.twn0 = lay.twn0;
+    t.ntwn = lay.ntwn;
+    t.nlt = lay.nlt;
+    t.ltn0 = lay.ltn0;
+    t.nltn = lay.nltn;
     t.p = &p;
     for (int i = threadIdx.x; i < lay.ntw; i += blockDim.x) t.tw[i] = p.tw[lay.tw0 + i];
+    for (int i = threadIdx.x; i < lay.ntwn; i += blockDim.x) t.tw[lay.ntw + i] = p.tw[lay.twn0 + i];
     for (int i = threadIdx.x; i < lay.nlp; i += blockDim.x) t.lp[i] = p.lp[lay.lp0 + i];
     for (int i = threadIdx.x; i < lay.npm; i += blockDim.x) t.pm[i] = p.perm[lay.pm0 + i];
+    for (int i = threadIdx.x; i < lay.nlt; i += blockDim.x) t.lt[i] = p.lpt[lay.lt0 + i];
+    for (int i = threadIdx.x; i < lay.nltn; i += blockDim.x) t.lt[lay.nlt + i] = p.lpt[lay.ltn0 + i];
     return t;
 }
 
@@ -348,6 +494,7 @@ __device__ __forceinline__ void fold1(const float2* __restrict__ X, const float*
     const int s = (S > 0) ? S : s_rt;
     const int items = nM1 * nN1;
     const int T = blockDim.x;
+    const wstfft::FastDiv dn(nN1);
     constexpr int U = (S == 1) ? 4 : (S == 2 ? 2 : 1);
     constexpr int UI = S > 0 ? S : 1, UJ = S > 0 ? S : 4;
     for (int it0 = threadIdx.x; it0 < items; it0 += U * T) {
@@ -359,7 +506,7 @@ __device__ __forceinline__ void fold1(const float2* __restrict__ X, const float*
             acc[k] = make_float2(0.f, 0.f);
             dst[k] = -1;
             if (it < items) {
-                const int u = it / nN1, v = it - (it / nN1) * nN1;
+                const int u = dn.div(it), v = it - u * nN1;
                 dst[k] = u * ld1 + v;
 #pragma unroll UI
                 for (int i = 0; i < s; ++i) {
@@ -391,38 +538,96 @@ __device__ __forceinline__ void fold1_any(int s1, const float2* X, const float* 
 //   B_b[u][v] = sum_{i,j < s} U1hat[u + i nM2][v + j nN2] * psi_b[...]
 // U1hat is read from the half spectrum H (nM1 x hld, columns 0..nN1/2):
 //   U1hat[kr][kc] = kc <= nN1/2 ? H[kr][kc] : conj(H[(nM1 - kr) % nM1][nN1 - kc]).
+// Box-sparse: only the aliases i in [i0, i0 + ni) (mod s) of row u and j in [j0, j0 + nj) of
+// column v are summed, where the pair's alias boxes (host: box_bins) cover every bin at which
+// either filter exceeds kBoxThreshold * its maximum; the dropped terms are below that bound.
 template <int S>
 __device__ __forceinline__ void fold2(const float2* H, int hld, int nM1, int nN1,
                                       const float2* __restrict__ psi2, long long pstride,
                                       int npair, int npath, float2* B, int pslot, int ld2, int nM2,
-                                      int nN2, int s_rt) {
+                                      int nN2, int s_rt, const int* __restrict__ box, int bstride) {
     const int s = (S > 0) ? S : s_rt;
+    const int smask = s - 1;
     const int half = nN1 >> 1;
     const int items = nM2 * nN2;
     const int total = npair * items;
-    constexpr int UI = S == 2 ? 2 : 1, UJ = S > 0 ? S : 2;
+    const wstfft::FastDiv ditems(items), dn(nN2);
     for (int w = threadIdx.x; w < total; w += blockDim.x) {
-        const int pr = w / items;
+        const int pr = ditems.div(w);
         const int it = w - pr * items;
-        const int u = it / nN2, v = it - (it / nN2) * nN2;
+        const int u = dn.div(it), v = it - u * nN2;
         const float2* ps = psi2 + pr * pstride;
+        const int* bx = box + pr * bstride;
+        const int rb = bx[u], cb = bx[nM2 + v];
+        const int i0 = rb & 255, ni = rb >> 8, j0 = cb & 255, nj = cb >> 8;
         float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
-#pragma unroll UI
-        for (int i = 0; i < s; ++i) {
-            const int kr = u + i * nM2;
+        auto row = [&](int i) {
+            const int kr = u + ((i0 + i) & smask) * nM2;
             const int krm = kr == 0 ? 0 : nM1 - kr;
             const float2* frow = ps + kr * nN1;
-#pragma unroll UJ
-            for (int j = 0; j < s; ++j) {
-                const int kc = v + j * nN2;
+            const float2* hrow = H + kr * hld;
+            const float2* hmir = H + krm * hld + nN1;
+            auto tap = [&](int j) {
+                const int kc = v + ((j0 + j) & smask) * nN2;
                 const bool mir = kc > half;
-                float2 a = H[mir ? krm * hld + (nN1 - kc) : kr * hld + kc];
+                float2 a = mir ? hmir[-kc] : hrow[kc];
                 a.y = mir ? -a.y : a.y;
                 const float2 f = frow[kc];
                 a0 = make_float2(fmaf(a.x, f.x, a0.x), fmaf(a.y, f.x, a0.y));
                 a1 = make_float2(fmaf(a.x, f.y, a1.x), fmaf(a.y, f.y, a1.y));
+            };
+            // predicated blocks of up to 4 aliases keep the filter loads of a block in flight
+            for (int jb = 0; jb < nj; jb += 4) {
+#pragma unroll
+                for (int j2 = 0; j2 < (S == 2 ? 2 : 4); ++j2)
+                    if (jb + j2 < nj) tap(jb + j2);
             }
+        };
+        for (int ib = 0; ib < ni; ib += 4) {
+#pragma unroll
+            for (int i2 = 0; i2 < (S == 2 ? 2 : 4); ++i2)
+                if (ib + i2 < ni) row(ib + i2);
         }
+        float2* dst = B + 2 * pr * pslot + u * ld2 + v;
+        dst[0] = a0;
+        if (2 * pr + 1 < npath) dst[pslot] = a1;
+    }
+}
+
+// s = 2 fold (j2 = j1 + 1, ~93 % of the alias box is significant, so dense): with nN2 = nN1 / 2
+// the four taps of (u, v) are rows u, u + nM2 and columns v (direct) and v + nN2 (the Hermitian
+// mirror conj(H[krm][nN2 - v]) for v > 0, H[kr][nN2] for v = 0); krm(u) = (nM1 - u) % nM1 and
+// krm(u + nM2) = nM2 - u.
+__device__ __forceinline__ void fold2_s2(const float2* H, int hld, int nM1, int nN1,
+                                         const float2* __restrict__ psi2, long long pstride,
+                                         int npair, int npath, float2* B, int pslot, int ld2,
+                                         int nM2, int nN2) {
+    const int items = nM2 * nN2;
+    const int total = npair * items;
+    const wstfft::FastDiv ditems(items), dn(nN2);
+    for (int w = threadIdx.x; w < total; w += blockDim.x) {
+        const int pr = ditems.div(w);
+        const int it = w - pr * items;
+        const int u = dn.div(it), v = it - u * nN2;
+        const float2* ps = psi2 + pr * pstride;
+        const int r0 = u, r1 = u + nM2;
+        const int m0 = u == 0 ? 0 : nM1 - u, m1 = nM2 - u;
+        // column v + nN2: mirrored index (nN2 - v) in row krm, or direct column nN2 when v == 0
+        const int cm = nN2 - v;
+        const int a01 = v == 0 ? r0 * hld + nN2 : m0 * hld + cm;
+        const int a11 = v == 0 ? r1 * hld + nN2 : m1 * hld + cm;
+        const float sg = v == 0 ? 1.f : -1.f;
+        const float2 h00 = H[r0 * hld + v], h10 = H[r1 * hld + v];
+        float2 h01 = H[a01], h11 = H[a11];
+        h01.y *= sg;
+        h11.y *= sg;
+        const float2 f00 = ps[r0 * nN1 + v], f01 = ps[r0 * nN1 + v + nN2];
+        const float2 f10 = ps[r1 * nN1 + v], f11 = ps[r1 * nN1 + v + nN2];
+        float2 a0, a1;
+        a0.x = fmaf(h00.x, f00.x, fmaf(h01.x, f01.x, fmaf(h10.x, f10.x, h11.x * f11.x)));
+        a0.y = fmaf(h00.y, f00.x, fmaf(h01.y, f01.x, fmaf(h10.y, f10.x, h11.y * f11.x)));
+        a1.x = fmaf(h00.x, f00.y, fmaf(h01.x, f01.y, fmaf(h10.x, f10.y, h11.x * f11.y)));
+        a1.y = fmaf(h00.y, f00.y, fmaf(h01.y, f01.y, fmaf(h10.y, f10.y, h11.y * f11.y)));
         float2* dst = B + 2 * pr * pslot + u * ld2 + v;
         dst[0] = a0;
         if (2 * pr + 1 < npath) dst[pslot] = a1;
@@ -432,10 +637,9 @@ __device__ __forceinline__ void fold2(const float2* H, int hld, int nM1, int nN1
 __device__ __forceinline__ void fold2_any(int s2, const float2* H, int hld, int nM1, int nN1,
                                           const float2* psi2, long long pstride, int npair,
                                           int npath, float2* B, int pslot, int ld2, int nM2,
-                                          int nN2) {
-    if (s2 == 2) fold2<2>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, 2);
-    else if (s2 == 4) fold2<4>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, 4);
-    else fold2<0>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, s2);
+                                          int nN2, const int* box, int bstride) {
+    if (s2 == 2) fold2_s2(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
+    else fold2<0>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, s2, box, bstride);
 }
 
 // XCD-aware decode of (plane, theta1) items: blocks b and b+8 share an XCD; give each XCD a
@@ -486,15 +690,21 @@ __global__ void __launch_bounds__(1024) k_prep(DevParams p, LdsLayout lay,
     }
     __syncthreads();
     wstfft::EpiIdentity id;
-    lds_fft2<FM, FN, wstfft::kMaxFamilyN, kNat, false>(A, 1, 0, PM, PN, ld, tb.twM(0), tb.twN(0), id);
+    lds_fft2<FM, FN, 0, wstfft::kMaxFamilyN, kNat, false>(A, 1, 0, PM, PN, ld, tb.twM(0), tb.twN(0), id);
     float2* dst = xhat + local * n;
     for (GridIter it(PN); it.u < PM; it.next()) dst[it.u * PN + it.v] = A[it.u * ld + it.v];
 }
 
+// Size classes of the k_o1 / k_o2 instantiations: CAP = largest level size of a launch
+// (max(PM, PN) >> j1).  SQ = 1: square plane whose order-2 low-pass fuses (fused_lowpass_ok), so
+// every level-j1 size is in (prev_cap(CAP), CAP] and the order-2 paths are <= CAP / 2: the
+// kernel carries only those FFTs (code size stays well inside the instruction cache).
+constexpr int prev_cap(int c) { return c <= 12 ? 0 : c <= 24 ? 12 : c <= 48 ? 24 : 48; }
+
 // ------------------------------------------------------------------------------------------
 // k_o1: one workgroup per (plane, theta1) at fixed j1 -- order 1 + half-spectrum export
 // ------------------------------------------------------------------------------------------
-template <int FM, int FN, int MAXN>
+template <int FM, int FN, int MAXN, int SQ>
 __global__ void __launch_bounds__(1024) k_o1(DevParams p, LdsLayout lay, int j1, int nimg,
                                              long long img0, const float2* __restrict__ xhat,
                                              float2* __restrict__ hexp, float* __restrict__ out,
@@ -524,7 +734,8 @@ __global__ void __launch_bounds__(1024) k_o1(DevParams p, LdsLayout lay, int j1,
     //    In place (digit-reversed rows and columns); the low-pass maps the permutation.
     EpiModulus mod1{1.f / (static_cast<float>(PM) * static_cast<float>(PN)), 0.f};
     if (!(dbg & 1))
-        lds_fft2<FM, FN, MAXN, kDR, true>(A, 1, 0, nM1, nN1, ld1, tb.twM(j1), tb.twN(j1), mod1);
+        lds_fft2<FM, FN, SQ ? prev_cap(MAXN) : 0, MAXN, kDR, true>(A, 1, 0, nM1, nN1, ld1, tb.twM(j1),
+                                                                  tb.twN(j1), mod1);
     const float mean1 = block_sum(mod1.sum, red) / n1;
 
     // 3. S1 at level j1, decimation 2^(J-j1)
@@ -545,7 +756,7 @@ __global__ void __launch_bounds__(1024) k_o1(DevParams p, LdsLayout lay, int j1,
     __syncthreads();
     wstfft::EpiIdentity id;
     if (!(dbg & 4))
-        lds_fft_lines<FN, MAXN, kRD, false>(A, wstfft::Lines{1, 0, nh, 2 * ld1, 1}, nN1,
+        lds_fft_lines<FN, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(A, wstfft::Lines{1, 0, nh, 2 * ld1, 1}, nN1,
                                             tb.twN(j1), id);
 
     // 5. split into the two rows' half spectra (columns 0..nN1/2) and export them
@@ -563,7 +774,7 @@ __global__ void __launch_bounds__(1024) k_o1(DevParams p, LdsLayout lay, int j1,
 // ------------------------------------------------------------------------------------------
 // k_o2: one workgroup per (plane, theta1) at fixed j1 -- all order-2 paths from U1hat
 // ------------------------------------------------------------------------------------------
-template <int FM, int FN, int MAXN>
+template <int FM, int FN, int MAXN, int SQ>
 __global__ void __launch_bounds__(1024) k_o2(DevParams p, LdsLayout lay, int j1, int nimg,
                                              long long img0, const float2* __restrict__ hexp,
                                              float* __restrict__ out, int pooled) {
@@ -588,7 +799,8 @@ __global__ void __launch_bounds__(1024) k_o2(DevParams p, LdsLayout lay, int j1,
     __syncthreads();
     wstfft::EpiIdentity id;
     if (!(dbg & 4))
-        lds_fft_lines<FM, MAXN, kRD, false>(H, wstfft::Lines{1, 0, hld, 1, hld}, nM1, tb.twM(j1), id);
+        lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(H, wstfft::Lines{1, 0, hld, 1, hld},
+                                                                     nM1, tb.twM(j1), id);
 
     // 2. order-2 paths in batches: Hermitian fold -> |ifft| -> S2 low-pass
     const int kbase = p.o2_base[j1 * L + l1];
@@ -604,17 +816,32 @@ __global__ void __launch_bounds__(1024) k_o2(DevParams p, LdsLayout lay, int j1,
             const int npair = (npath + 1) >> 1;
             const float2* ps = p.psi2 + p.psi2_off[(j2 * J + j1) * nq + (l2a >> 1)];
             const long long pstride = static_cast<long long>(n1);
+            const int* bx = p.box + p.box_off[j2 * J + j1] + (l2a >> 1) * (nM2 + nN2);
             if (!(dbg & 8))
-                fold2_any(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
+                fold2_any(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
+                          bx, nM2 + nN2);
             __syncthreads();
-            EpiModulus mod2{1.f / static_cast<float>(n1), 0.f};
-            if (!(dbg & 16))
-                lds_fft2<FM, FN, MAXN, kDR, true>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
-                                                  tb.twN(j2), mod2);
-            if (!(dbg & 64)) {
-                lds_lowpass(B, npath, pslot, nM2, nN2, ld2, tb.lpM(j2), tb.lpN(j2), tb.pmM(j2),
-                            tb.pmN(j2), 1 << (J - j2), p.oM, p.oN, S);
+            const float scale2 = 1.f / static_cast<float>(n1);
+            if constexpr (SQ) {
+                // rows, then the column pass fused with |.| and the S2 low-pass
+                if (!(dbg & 16))
+                    lds_fft_lines<FN, 0, MAXN / 2, kDR, true>(
+                        B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, nN2, tb.twN(j2), id);
+                if (!(dbg & 64))
+                    family_cols_modlp<FM, 0, MAXN / 2>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
+                                                       tb.gM(j2), tb.gN(j2), lay.oms, p.oM, p.oN,
+                                                       scale2, S);
                 emit(S, npath, kbase + (j2 - j1 - 1) * L + l2a, img, p.K, p.oM, p.oN, out, pooled);
+            } else {
+                EpiModulus mod2{scale2, 0.f};
+                if (!(dbg & 16))
+                    lds_fft2<FM, FN, 0, MAXN, kDR, true>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
+                                                         tb.twN(j2), mod2);
+                if (!(dbg & 64)) {
+                    lds_lowpass(B, npath, pslot, nM2, nN2, ld2, tb.lpM(j2), tb.lpN(j2), tb.pmM(j2),
+                                tb.pmN(j2), 1 << (J - j2), p.oM, p.oN, S);
+                    emit(S, npath, kbase + (j2 - j1 - 1) * L + l2a, img, p.K, p.oM, p.oN, out, pooled);
+                }
             }
             __syncthreads();
         }

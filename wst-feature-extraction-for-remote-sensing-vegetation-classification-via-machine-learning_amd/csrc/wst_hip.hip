@@ -20,16 +20,15 @@
 #include <vector>
 
 #include "filter_bank.h"
-#include "wst_device.h"
 #include "wst_hip.h"
+#include "wst_launch.h"
 
 using wstdev::DevParams;
 using wstdev::LdsLayout;
-using wstdev::k_o1;
-using wstdev::k_o2;
-using wstdev::k_prep;
 using wstdev::kMaxLds;
 using wstdev::odd_ld;
+using wstlaunch::FamilyOps;
+using wstlaunch::Launch;
 
 namespace {
 
@@ -48,15 +47,8 @@ int fail(int code, const std::string& msg) {
     } while (0)
 
 // ------------------------------------------------------------------------------------------
-// size-family instantiations
+// size families (kernels are compiled per pair of families: wst_kernels.hip, wst_launch.h)
 // ------------------------------------------------------------------------------------------
-// Every level size of a plan is (odd part of P) * 2^k, so kernels are compiled per pair of size
-// families (rows, columns); family 0 = generic O(n) DFT for sizes outside the compiled set.
-#define WST_FAMILY_PAIRS(X) X(0, 0) X(1, 1) X(3, 3) X(5, 5) X(9, 9) X(17, 17) X(3, 1) X(1, 3)
-// size caps of the k_o1 / k_o2 instantiations (largest FFT a launch needs = max(PM, PN) >> j1):
-// a cap bounds the unrolled transforms a kernel carries, hence its register footprint
-#define WST_CAPS(Y, A, B) Y(A, B, 12) Y(A, B, 24) Y(A, B, 48) Y(A, B, 136)
-
 int odd_part(int n) {
     while (n > 0 && (n % 2) == 0) n /= 2;
     return n;
@@ -66,74 +58,14 @@ int family_of(int P) {
     const bool compiled = (o == 1 || o == 3 || o == 5 || o == 9 || o == 17);
     return (compiled && P <= wstfft::kMaxFamilyN) ? o : 0;
 }
-bool pair_compiled(int fm, int fn) {
-#define WST_PAIR_EQ(A, B) if (fm == A && fn == B) return true;
-    WST_FAMILY_PAIRS(WST_PAIR_EQ)
-#undef WST_PAIR_EQ
-    return false;
+const FamilyOps* family_ops(int fm, int fn) {
+#define WST_PAIR_OPS(A, B) \
+    if (fm == A && fn == B) return &wstlaunch::WST_FAMILY_GETTER(A, B)();
+    WST_FAMILY_PAIRS(WST_PAIR_OPS)
+#undef WST_PAIR_OPS
+    return nullptr;
 }
 int cap_for(int n) { return n <= 12 ? 12 : n <= 24 ? 24 : n <= 48 ? 48 : 136; }
-
-int set_lds_attributes() {
-#define WST_CAP_ATTR(A, B, C)                                                                    \
-    WST_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_o1<A, B, C>),             \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));    \
-    WST_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_o2<A, B, C>),             \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));
-#define WST_PAIR_ATTR(A, B)                                                                      \
-    WST_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(k_prep<A, B>),              \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, kMaxLds));    \
-    WST_CAPS(WST_CAP_ATTR, A, B)
-    WST_FAMILY_PAIRS(WST_PAIR_ATTR)
-#undef WST_PAIR_ATTR
-#undef WST_CAP_ATTR
-    return WST_OK;
-}
-
-struct Launch {
-    dim3 grid, block;
-    size_t lds;
-    hipStream_t st;
-};
-
-void launch_prep(int fm, int fn, const Launch& q, const DevParams& dp, const LdsLayout& lay,
-                 const float* in, long long img0, float2* xhat, float* out, int pooled) {
-#define WST_PAIR_PREP(A, B)                                                                      \
-    if (fm == A && fn == B) {                                                                    \
-        hipLaunchKernelGGL((k_prep<A, B>), q.grid, q.block, q.lds, q.st, dp, lay, in, img0, xhat, \
-                           out, pooled);                                                         \
-        return;                                                                                  \
-    }
-    WST_FAMILY_PAIRS(WST_PAIR_PREP)
-#undef WST_PAIR_PREP
-}
-void launch_o1(int fm, int fn, int cap, const Launch& q, const DevParams& dp, const LdsLayout& lay,
-               int j1, int nimg, long long img0, const float2* xhat, float2* hexp, float* out,
-               int pooled) {
-#define WST_O1_LAUNCH(A, B, C)                                                                   \
-    if (fm == A && fn == B && cap == C) {                                                        \
-        hipLaunchKernelGGL((k_o1<A, B, C>), q.grid, q.block, q.lds, q.st, dp, lay, j1, nimg, img0, \
-                           xhat, hexp, out, pooled);                                             \
-        return;                                                                                  \
-    }
-#define WST_PAIR_O1(A, B) WST_CAPS(WST_O1_LAUNCH, A, B)
-    WST_FAMILY_PAIRS(WST_PAIR_O1)
-#undef WST_PAIR_O1
-#undef WST_O1_LAUNCH
-}
-void launch_o2(int fm, int fn, int cap, const Launch& q, const DevParams& dp, const LdsLayout& lay,
-               int j1, int nimg, long long img0, const float2* hexp, float* out, int pooled) {
-#define WST_O2_LAUNCH(A, B, C)                                                                   \
-    if (fm == A && fn == B && cap == C) {                                                        \
-        hipLaunchKernelGGL((k_o2<A, B, C>), q.grid, q.block, q.lds, q.st, dp, lay, j1, nimg, img0, \
-                           hexp, out, pooled);                                                   \
-        return;                                                                                  \
-    }
-#define WST_PAIR_O2(A, B) WST_CAPS(WST_O2_LAUNCH, A, B)
-    WST_FAMILY_PAIRS(WST_PAIR_O2)
-#undef WST_PAIR_O2
-#undef WST_O2_LAUNCH
-}
 
 size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
@@ -175,8 +107,14 @@ struct wst_plan {
     int* d_perm_off = nullptr;
     float2* d_psi2 = nullptr;
     long long* d_psi2_off = nullptr;
+    int* d_box = nullptr;
+    int* d_box_off = nullptr;
+    float* d_lpt = nullptr;
+    int* d_lpt_off = nullptr;
     // launch geometry
     int fam_m = 0, fam_n = 0;   // FFT size families (odd part of PM / PN), 0 = generic DFT
+    const FamilyOps* ops = nullptr;
+    int sq = 0;                 // square plane with the fused order-2 low-pass (k_o1/k_o2 SQ=1)
     int prep_threads = 256;
     size_t prep_lds = 0;
     LdsLayout prep_lay{};
@@ -208,6 +146,10 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_perm_off);
     (void)hipFree(p->d_psi2);
     (void)hipFree(p->d_psi2_off);
+    (void)hipFree(p->d_box);
+    (void)hipFree(p->d_box_off);
+    (void)hipFree(p->d_lpt);
+    (void)hipFree(p->d_lpt_off);
     if (p->ws) (void)hipFree(p->ws);
     delete p;
 }
@@ -224,15 +166,25 @@ int upload(T** dst, const std::vector<T>& src) {
 // levels [r_tw0, r_tw1] (twiddles), [r_lp0, r_lp1] (low-pass taps, permutations), S and the
 // reduction scratch.  An empty range has r0 > r1.
 struct TableOffsets {
-    std::vector<int> tw_off, lp_off, perm_off;   // each with a trailing total
+    std::vector<int> tw_off, lp_off, perm_off, lpt_off;   // each with a trailing total
+    std::vector<int> tw_len, lpt_len;                      // table lengths ([2r + d])
 };
 
-size_t layout(LdsLayout& lay, size_t data_a, size_t data_b, const TableOffsets& t, int r_tw0,
-              int r_tw1, int r_lp0, int r_lp1, size_t s_floats) {
+// Table blocks per kernel: levels [r0, r1] of the twiddle and tap-matrix pools, whose M-side
+// and N-side tables are stored as two blocks (all M levels, then all N levels); a square kernel
+// (n_side = false) loads only the M block and reads it for both dimensions.
+struct Blocks {
+    int r0 = 1, r1 = 0;
+    bool n_side = true;
+};
+
+size_t layout(LdsLayout& lay, size_t data_a, size_t data_b, const TableOffsets& t, Blocks tw,
+              int r_lp0, int r_lp1, size_t s_floats, Blocks lt = Blocks{}, int oms = 4) {
     size_t o = align16(data_a);
     lay.off_b = static_cast<int>(o);
     o += align16(data_b);
     lay.bcap = static_cast<int>(data_b / sizeof(float2));
+    lay.oms = oms;
     auto slice = [](const std::vector<int>& off, int r0, int r1, int& base, int& n) {
         if (r0 > r1) {
             base = 0;
@@ -242,15 +194,31 @@ size_t layout(LdsLayout& lay, size_t data_a, size_t data_b, const TableOffsets& 
         base = off[2 * r0];
         n = off[2 * r1 + 2] - base;
     };
-    slice(t.tw_off, r_tw0, r_tw1, lay.tw0, lay.ntw);
+    // one side's levels [r0, r1]: tables of that side are contiguous in level order
+    auto side = [](const std::vector<int>& off, const std::vector<int>& len, Blocks b, int d,
+                   int& base, int& n) {
+        if (b.r0 > b.r1 || (d == 1 && !b.n_side)) {
+            base = 0;
+            n = 0;
+            return;
+        }
+        base = off[2 * b.r0 + d];
+        n = off[2 * b.r1 + d] + len[2 * b.r1 + d] - base;
+    };
+    side(t.tw_off, t.tw_len, tw, 0, lay.tw0, lay.ntw);
+    side(t.tw_off, t.tw_len, tw, 1, lay.twn0, lay.ntwn);
     slice(t.lp_off, r_lp0, r_lp1, lay.lp0, lay.nlp);
     slice(t.perm_off, r_lp0, r_lp1, lay.pm0, lay.npm);
+    side(t.lpt_off, t.lpt_len, lt, 0, lay.lt0, lay.nlt);
+    side(t.lpt_off, t.lpt_len, lt, 1, lay.ltn0, lay.nltn);
     lay.off_tw = static_cast<int>(o);
-    o += align16(static_cast<size_t>(lay.ntw) * sizeof(float2));
+    o += align16(static_cast<size_t>(lay.ntw + lay.ntwn) * sizeof(float2));
     lay.off_lp = static_cast<int>(o);
     o += align16(static_cast<size_t>(lay.nlp) * sizeof(float));
     lay.off_pm = static_cast<int>(o);
     o += align16(static_cast<size_t>(lay.npm) * sizeof(int));
+    lay.off_lt = static_cast<int>(o);
+    o += align16(static_cast<size_t>(lay.nlt + lay.nltn) * sizeof(float));
     lay.off_s = static_cast<int>(o);
     o += align16(s_floats * sizeof(float));
     lay.off_red = static_cast<int>(o);
@@ -263,6 +231,39 @@ int paths_per_batch(size_t bcap, size_t pslot, int L) {
     const int nq = (L + 1) / 2;
     int pb = static_cast<int>(bcap / pslot);
     return std::max(2, std::min(pb & ~1, 2 * nq));
+}
+
+// Rows per unit of the last (column) stage of an in-place transform of size n.
+int rows_per_unit(int n) {
+    const int n2 = wstfft::split_n2(n);
+    return n2 == 1 ? n : n2;
+}
+
+// Bins of an order-2 filter pair below this fraction of the filter's maximum are skipped by the
+// box-sparse fold (dropped contribution < 1e-10 relative; measured 5e-11 in float64 at c2).
+constexpr double kBoxThreshold = 1e-10;
+
+// Minimal cyclic window [i0, i0 + n) of Z_s covering the set bits of `hit` -> i0 | n << 8.
+int cyclic_window(const std::vector<char>& hit) {
+    const int s = static_cast<int>(hit.size());
+    std::vector<int> on;
+    for (int i = 0; i < s; ++i)
+        if (hit[i]) on.push_back(i);
+    if (on.empty()) return 0;
+    if (static_cast<int>(on.size()) == s) return s << 8;
+    // the window starts after the largest cyclic gap between consecutive set positions
+    int best_gap = -1, start = on[0];
+    for (size_t k = 0; k < on.size(); ++k) {
+        const int a = on[k], b = on[(k + 1) % on.size()];
+        const int gap = ((b - a) % s + s) % s;
+        const int g = (on.size() == 1) ? s : gap;
+        if (g > best_gap) {
+            best_gap = g;
+            start = b;
+        }
+    }
+    const int len = s - best_gap + 1;
+    return start | (len << 8);
 }
 
 }  // namespace
@@ -294,7 +295,11 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
 
     plan->fam_m = family_of(g.PM);
     plan->fam_n = family_of(g.PN);
-    if (!pair_compiled(plan->fam_m, plan->fam_n)) plan->fam_m = plan->fam_n = 0;
+    plan->ops = family_ops(plan->fam_m, plan->fam_n);
+    if (!plan->ops) {
+        plan->fam_m = plan->fam_n = 0;
+        plan->ops = family_ops(0, 0);
+    }
 
     TableOffsets t;
     // digit-reversal maps of the in-place transforms (identity for the generic DFT)
@@ -355,12 +360,74 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
                     }
                 }
     }
+    // alias boxes of the order-2 pairs (see fold2): per (j2, r) all pairs, stride nM2 + nN2
+    std::vector<int> box;
+    std::vector<int> box_off(static_cast<size_t>(J) * J, 0);
+    if (max_order >= 2) {
+        for (int j2 = 1; j2 < J; ++j2)
+            for (int r = 0; r < j2 && r < wst::psi_levels(j2, J); ++r) {
+                box_off[static_cast<size_t>(j2) * J + r] = static_cast<int>(box.size());
+                const int nM1 = g.PM >> r, nN1 = g.PN >> r, nM2 = g.PM >> j2, nN2 = g.PN >> j2;
+                const int sa = 1 << (j2 - r);
+                for (int q = 0; q < nq; ++q) {
+                    std::vector<char> rsig(nM1, 0), csig(nN1, 0);
+                    for (int u = 0; u < 2; ++u) {
+                        const int l2 = 2 * q + u;
+                        if (l2 >= L) continue;
+                        const auto& f = fb.psi[static_cast<size_t>(j2) * L + l2][r];
+                        double mx = 0.0;
+                        for (double v : f) mx = std::max(mx, std::fabs(v));
+                        for (int kr = 0; kr < nM1; ++kr)
+                            for (int kc = 0; kc < nN1; ++kc)
+                                if (std::fabs(f[static_cast<size_t>(kr) * nN1 + kc]) > kBoxThreshold * mx) {
+                                    rsig[kr] = 1;
+                                    csig[kc] = 1;
+                                }
+                    }
+                    if (const char* e = std::getenv("WST_BOX"))   // 0: dense fold (A/B timing)
+                        if (std::atoi(e) == 0) std::fill(rsig.begin(), rsig.end(), 1), std::fill(csig.begin(), csig.end(), 1);
+                    std::vector<char> hit(sa);
+                    for (int u = 0; u < nM2; ++u) {
+                        for (int i = 0; i < sa; ++i) hit[i] = rsig[u + i * nM2];
+                        box.push_back(cyclic_window(hit));
+                    }
+                    for (int v = 0; v < nN2; ++v) {
+                        for (int i = 0; i < sa; ++i) hit[i] = csig[v + i * nN2];
+                        box.push_back(cyclic_window(hit));
+                    }
+                }
+            }
+    }
+    // low-pass tap matrices in physical (digit-reversed) order, unpad + decimation folded in:
+    //   GM_r[p][a] = hM_r[(s (a + 1) - perm_r(p)) mod n], s = 2^(J - r); rows padded to oms floats.
+    //   Pool order: GM_0 .. GM_{J-1}, then GN_0 .. GN_{J-1} (see Blocks).
+    const int oms = std::max(g.oM, g.oN) <= 4 ? 4 : wstdev::kLpOM;
+    std::vector<float> lpt;
+    t.lpt_off.assign(2 * static_cast<size_t>(J) + 1, 0);
+    t.lpt_len.assign(2 * static_cast<size_t>(J), 0);
+    for (int d = 0; d < 2; ++d)
+        for (int r = 0; r < J; ++r) {
+            const int n = (d == 0 ? g.PM : g.PN) >> r;
+            const int no = d == 0 ? g.oM : g.oN;
+            const int sdec = 1 << (J - r);
+            const auto& h = d == 0 ? fb.hM[r] : fb.hN[r];
+            const int* pm = perm.data() + t.perm_off[2 * r + d];
+            t.lpt_off[2 * r + d] = static_cast<int>(lpt.size());
+            for (int p = 0; p < n; ++p)
+                for (int a = 0; a < oms; ++a)
+                    lpt.push_back(a < no ? static_cast<float>(h[((sdec * (a + 1) - pm[p]) % n + n) % n]) : 0.f);
+            t.lpt_len[2 * r + d] = n * oms;
+        }
+    t.lpt_off.back() = static_cast<int>(lpt.size());
+    // twiddles exp(-2 pi i k / n) per level and side; pool order: M levels 0..J, then N levels
     std::vector<float2> tw;
-    t.tw_off.resize(2 * static_cast<size_t>(J + 1) + 1);
-    for (int r = 0; r <= J; ++r)
-        for (int d = 0; d < 2; ++d) {
+    t.tw_off.assign(2 * static_cast<size_t>(J + 1) + 1, 0);
+    t.tw_len.assign(2 * static_cast<size_t>(J + 1), 0);
+    for (int d = 0; d < 2; ++d)
+        for (int r = 0; r <= J; ++r) {
             const int n = (d == 0 ? g.PM : g.PN) >> r;
             t.tw_off[2 * r + d] = static_cast<int>(tw.size());
+            t.tw_len[2 * r + d] = n;
             for (int k = 0; k < n; ++k) {
                 const double a = 2.0 * 3.14159265358979323846 * k / n;
                 tw.push_back(make_float2(static_cast<float>(std::cos(a)), static_cast<float>(-std::sin(a))));
@@ -389,6 +456,10 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     if ((rc = upload(&plan->d_psi2_off, psi2_off)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_perm, perm)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_perm_off, t.perm_off)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_box, box)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_box_off, box_off)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_lpt, lpt)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_lpt_off, t.lpt_off)) != WST_OK) return rc;
 
     DevParams& dp = plan->dp;
     dp.M = g.M; dp.N = g.N; dp.PM = g.PM; dp.PN = g.PN; dp.J = J; dp.L = L;
@@ -398,9 +469,6 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     {
         const char* dbg = std::getenv("WST_DEBUG_SKIP");
         dp.dbg_skip = dbg ? std::atoi(dbg) : 0;
-        const char* dfft = std::getenv("WST_DEBUG_FFT");
-        const int v = dfft ? std::atoi(dfft) : 0;
-        WST_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(wstfft::g_dbg_fft), &v, sizeof(int)));
     }
     dp.psi = plan->d_psi; dp.psi_off = plan->d_psi_off;
     dp.lp = plan->d_lp; dp.lp_off = plan->d_lp_off;
@@ -408,6 +476,15 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     dp.perm = plan->d_perm; dp.perm_off = plan->d_perm_off;
     dp.o2_base = plan->d_o2;
     dp.psi2 = plan->d_psi2; dp.psi2_off = plan->d_psi2_off;
+    dp.box = plan->d_box; dp.box_off = plan->d_box_off;
+    dp.lpt = plan->d_lpt; dp.lpt_off = plan->d_lpt_off;
+    // square variant (bounded FFT sizes + fused order-2 low-pass): square plane of a compiled
+    // family, oM <= kLpOM and every order-2 level's column units hold ceil(oM / 2) slots
+    plan->sq = (plan->fam_m > 0 && plan->fam_m == plan->fam_n && g.PM == g.PN &&
+                g.oM <= wstdev::kLpOM) ? 1 : 0;
+    for (int j2 = 1; j2 < J; ++j2)
+        if (rows_per_unit(g.PM >> j2) < (g.oM + 1) / 2) plan->sq = 0;
+    if (const char* e = std::getenv("WST_SQ")) plan->sq = plan->sq && std::atoi(e) != 0;
 
     // --- LDS layouts ---
     const size_t omn = static_cast<size_t>(g.oM) * g.oN;
@@ -418,7 +495,7 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
                         " exceeds the LDS-resident path (160 KiB per CU)");
     };
     plan->prep_lds = layout(plan->prep_lay, static_cast<size_t>(g.PM) * odd_ld(g.PN) * sizeof(float2),
-                            0, t, 0, 0, 0, 0, omn);
+                            0, t, Blocks{0, 0, true}, 0, 0, omn);
     plan->prep_lay.npm = 0;   // k_prep works in natural order
     if (plan->prep_lds > static_cast<size_t>(kMaxLds)) return too_big("k_prep", 0);
     plan->prep_threads = static_cast<size_t>(g.PM) * g.PN >= 4096 ? 512 : 256;
@@ -441,7 +518,7 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
         plan->o1_threads[j1] = default_threads(n1);
         plan->o2_threads[j1] = default_threads(n1);
         plan->o1_lds[j1] = layout(plan->o1_lay[j1], static_cast<size_t>(nM1) * odd_ld(nN1) * sizeof(float2),
-                                  0, t, j1, j1, j1, j1, omn);
+                                  0, t, Blocks{j1, j1, !plan->sq}, j1, j1, omn);
         if (plan->o1_lds[j1] > static_cast<size_t>(kMaxLds)) return too_big("k_o1", j1);
         if (!do2) continue;
         if (nM1 % 2 != 0 || nN1 % 2 != 0)
@@ -456,14 +533,28 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
         size_t smax = 0;
         for (int j2 = j1 + 1; j2 < J; ++j2)
             smax = std::max(smax, static_cast<size_t>(paths_per_batch(bcap, pslot(j2), L)) * omn);
-        plan->o2_lds[j1] = layout(plan->o2_lay[j1], static_cast<size_t>(nM1) * hld * sizeof(float2),
-                                  bcap * sizeof(float2), t, j1, J - 1, j1 + 1, J - 1, smax);
+        if (plan->sq)   // tap matrices replace the 1-D taps and permutations; M-side tables only
+            plan->o2_lds[j1] = layout(plan->o2_lay[j1], static_cast<size_t>(nM1) * hld * sizeof(float2),
+                                      bcap * sizeof(float2), t, Blocks{j1, J - 1, false}, 1, 0, smax,
+                                      Blocks{j1 + 1, J - 1, false}, oms);
+        else
+            plan->o2_lds[j1] = layout(plan->o2_lay[j1], static_cast<size_t>(nM1) * hld * sizeof(float2),
+                                      bcap * sizeof(float2), t, Blocks{j1, J - 1, true}, j1 + 1, J - 1,
+                                      smax);
         if (plan->o2_lds[j1] > static_cast<size_t>(kMaxLds)) return too_big("k_o2", j1);
     }
     plan->ws_plane = align16(wsp);
+    if (std::getenv("WST_VERBOSE")) {
+        std::fprintf(stderr, "[wst] plan %dx%d J=%d L=%d P=%dx%d fam=(%d,%d) sq=%d prep_lds=%zu\n", M, N, J, L,
+                     g.PM, g.PN, plan->fam_m, plan->fam_n, plan->sq, plan->prep_lds);
+        for (int j1 = 0; j1 < J; ++j1)
+            std::fprintf(stderr, "[wst]   j1=%d cap=%d o1: %d thr %zu B   o2: %d thr %zu B\n", j1,
+                         plan->cap[j1], plan->o1_threads[j1], plan->o1_lds[j1], plan->o2_threads[j1],
+                         plan->o2_lds[j1]);
+    }
     threads_override("WST_O1_THREADS", plan->o1_threads);
     threads_override("WST_O2_THREADS", plan->o2_threads);
-    if ((rc = set_lds_attributes()) != WST_OK) return rc;
+    WST_HIP_CHECK(plan->ops->set_attrs());
 
     *out = plan.release();
     g_last_error.clear();
@@ -582,25 +673,24 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
         const int nimg = static_cast<int>(std::min<int64_t>(chunk, nbatch - c0));
         const long long img0 = static_cast<long long>(c0);
         if ((rc = timer.begin(stream)) != WST_OK) return rc;
-        launch_prep(plan->fam_m, plan->fam_n,
-                    Launch{dim3(nimg), dim3(plan->prep_threads), plan->prep_lds, stream}, plan->dp,
-                    plan->prep_lay, d_in + c0 * inM * inN, img0, xhat, d_out, pooled);
+        plan->ops->prep(Launch{dim3(nimg), dim3(plan->prep_threads), plan->prep_lds, stream},
+                        plan->dp, plan->prep_lay, d_in + c0 * inM * inN, img0, xhat, d_out, pooled);
         WST_HIP_CHECK(hipGetLastError());
         if ((rc = timer.end(stream, 0)) != WST_OK) return rc;
         for (int j1 = 0; j1 < g.J; ++j1) {
             const bool do2 = g.max_order >= 2 && j1 < g.J - 1;
             float2* hexp = do2 ? reinterpret_cast<float2*>(base + plan->ws_h_off[j1] * chunk) : nullptr;
             if ((rc = timer.begin(stream)) != WST_OK) return rc;
-            launch_o1(plan->fam_m, plan->fam_n, plan->cap[j1],
-                      Launch{dim3(nimg * g.L), dim3(plan->o1_threads[j1]), plan->o1_lds[j1], stream},
-                      plan->dp, plan->o1_lay[j1], j1, nimg, img0, xhat, hexp, d_out, pooled);
+            plan->ops->o1(plan->cap[j1], plan->sq,
+                          Launch{dim3(nimg * g.L), dim3(plan->o1_threads[j1]), plan->o1_lds[j1], stream},
+                          plan->dp, plan->o1_lay[j1], j1, nimg, img0, xhat, hexp, d_out, pooled);
             WST_HIP_CHECK(hipGetLastError());
             if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
             if (!do2) continue;
             if ((rc = timer.begin(stream)) != WST_OK) return rc;
-            launch_o2(plan->fam_m, plan->fam_n, plan->cap[j1],
-                      Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
-                      plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled);
+            plan->ops->o2(plan->cap[j1], plan->sq,
+                          Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
+                          plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled);
             WST_HIP_CHECK(hipGetLastError());
             if ((rc = timer.end(stream, 1 + g.J + j1)) != WST_OK) return rc;
         }

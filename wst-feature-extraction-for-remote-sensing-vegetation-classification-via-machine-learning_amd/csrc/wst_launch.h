@@ -1,0 +1,41 @@
+// Launch table between the host plan code (wst_hip.hip) and the kernel instantiations, which are
+// compiled per FFT size-family pair in separate translation units (wst_kernels.hip built once per
+// pair by the Makefile) so the build runs in parallel and each object carries one family's code.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "wst_device.h"
+
+namespace wstlaunch {
+
+struct Launch {
+    dim3 grid, block;
+    size_t lds;
+    hipStream_t st;
+};
+
+using wstdev::DevParams;
+using wstdev::LdsLayout;
+
+struct FamilyOps {
+    int fm, fn;
+    // raise every kernel's dynamic-LDS limit to the full 160 KiB
+    hipError_t (*set_attrs)();
+    void (*prep)(const Launch&, const DevParams&, const LdsLayout&, const float* in, long long img0,
+                 float2* xhat, float* out, int pooled);
+    // cap: size class (12/24/48/136); sq: square fused variant (only for fm == fn > 0)
+    void (*o1)(int cap, int sq, const Launch&, const DevParams&, const LdsLayout&, int j1, int nimg,
+               long long img0, const float2* xhat, float2* hexp, float* out, int pooled);
+    void (*o2)(int cap, int sq, const Launch&, const DevParams&, const LdsLayout&, int j1, int nimg,
+               long long img0, const float2* hexp, float* out, int pooled);
+};
+
+// The compiled family pairs (rows, columns); family 0 = generic O(n) DFT.
+#define WST_FAMILY_PAIRS(X) X(0, 0) X(1, 1) X(3, 3) X(5, 5) X(9, 9) X(17, 17) X(3, 1) X(1, 3)
+#define WST_FAMILY_GETTER(A, B) wst_family_ops_##A##_##B
+#define WST_DECLARE_GETTER(A, B) const FamilyOps& WST_FAMILY_GETTER(A, B)();
+WST_FAMILY_PAIRS(WST_DECLARE_GETTER)
+#undef WST_DECLARE_GETTER
+
+}  // namespace wstlaunch
