@@ -53,6 +53,9 @@ struct DevParams {
                                   // entries (first alias | count << 8); pairs of one (j2, r)
                                   // contiguous, stride box_stride[j2]
     const int* box_off;           // [j2*J + r] -> first pair's entries
+    const int* box1_off;          // order-1 boxes (same pool, s >= 4): [j*L + l] -> nM1 + nN1
+                                  // entries of psi_{j,l} at level 0, -1 = dense
+    int box1_min_s;               // smallest order-1 alias count using the box-sparse fold
     const float* lpt;             // low-pass tap matrices in physical (digit-reversed) order:
     const int* lpt_off;           // [2r] GM_r (PM>>r rows x kLpOM), [2r+1] GN_r (PN>>r x oN)
 };
@@ -526,10 +529,45 @@ __device__ __forceinline__ void fold1(const float2* __restrict__ X, const float*
     }
 }
 
+// Box-sparse order-1 fold (s >= 4): aliases i in [i0, i0 + ni) of row u and j in [j0, j0 + nj) of
+// column v only (see fold2 / box tables); predicated blocks of 4 keep the loads in flight.
+__device__ __forceinline__ void fold1_box(const float2* __restrict__ X, const float* __restrict__ psi0,
+                                          int PN, float2* A, int ld1, int nM1, int nN1, int s,
+                                          const int* __restrict__ box) {
+    const int items = nM1 * nN1;
+    const int smask = s - 1;
+    const wstfft::FastDiv dn(nN1);
+    for (int it = threadIdx.x; it < items; it += blockDim.x) {
+        const int u = dn.div(it), v = it - u * nN1;
+        const int rb = box[u], cb = box[nM1 + v];
+        const int i0 = rb & 255, ni = rb >> 8, j0 = cb & 255, nj = cb >> 8;
+        float2 acc = make_float2(0.f, 0.f);
+        for (int ib = 0; ib < ni; ib += 4) {
+#pragma unroll
+            for (int i2 = 0; i2 < 4; ++i2) {
+                if (ib + i2 >= ni) continue;
+                const int rowoff = (u + ((i0 + ib + i2) & smask) * nM1) * PN + v;
+                for (int jb = 0; jb < nj; jb += 4) {
+#pragma unroll
+                    for (int j2 = 0; j2 < 4; ++j2) {
+                        if (jb + j2 >= nj) continue;
+                        const int idx = rowoff + ((j0 + jb + j2) & smask) * nN1;
+                        const float f = psi0[idx];
+                        const float2 xv = X[idx];
+                        acc = make_float2(fmaf(xv.x, f, acc.x), fmaf(xv.y, f, acc.y));
+                    }
+                }
+            }
+        }
+        A[u * ld1 + v] = acc;
+    }
+}
+
 __device__ __forceinline__ void fold1_any(int s1, const float2* X, const float* psi0, int PN,
-                                          float2* A, int ld1, int nM1, int nN1) {
+                                          float2* A, int ld1, int nM1, int nN1, const int* box) {
     if (s1 == 1) fold1<1>(X, psi0, PN, A, ld1, nM1, nN1, 1);
     else if (s1 == 2) fold1<2>(X, psi0, PN, A, ld1, nM1, nN1, 2);
+    else if (box) fold1_box(X, psi0, PN, A, ld1, nM1, nN1, s1, box);
     else if (s1 == 4) fold1<4>(X, psi0, PN, A, ld1, nM1, nN1, 4);
     else fold1<0>(X, psi0, PN, A, ld1, nM1, nN1, s1);
 }
@@ -727,7 +765,9 @@ __global__ void __launch_bounds__(1024) k_o1(DevParams p, LdsLayout lay, int j1,
     // 1. fold_{2^j1}(Xhat * psi0_{j1,l1}) straight from HBM/L2
     const float* psi0 = p.psi + p.psi_off[(j1 * L + l1) * J + 0];
     const float2* X = xhat + static_cast<long long>(local) * PM * PN;
-    if (!(dbg & 128)) fold1_any(1 << j1, X, psi0, PN, A, ld1, nM1, nN1);
+    const int b1 = p.box1_off[j1 * L + l1];
+    const bool use_box1 = b1 >= 0 && (1 << j1) >= p.box1_min_s;
+    if (!(dbg & 128)) fold1_any(1 << j1, X, psi0, PN, A, ld1, nM1, nN1, use_box1 ? p.box + b1 : nullptr);
     __syncthreads();
 
     // 2. U1 = |ifft(.)|, modulus fused into the last pass; fold-mean + ifft scale = 1/(PM PN).

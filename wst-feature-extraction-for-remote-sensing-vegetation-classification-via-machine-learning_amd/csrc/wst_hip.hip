@@ -109,6 +109,7 @@ struct wst_plan {
     long long* d_psi2_off = nullptr;
     int* d_box = nullptr;
     int* d_box_off = nullptr;
+    int* d_box1_off = nullptr;
     float* d_lpt = nullptr;
     int* d_lpt_off = nullptr;
     // launch geometry
@@ -148,6 +149,7 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_psi2_off);
     (void)hipFree(p->d_box);
     (void)hipFree(p->d_box_off);
+    (void)hipFree(p->d_box1_off);
     (void)hipFree(p->d_lpt);
     (void)hipFree(p->d_lpt_off);
     if (p->ws) (void)hipFree(p->ws);
@@ -398,6 +400,34 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
                 }
             }
     }
+    // order-1 alias boxes (psi_{j,l} at level 0 folded by s = 2^j; s >= 4 only)
+    std::vector<int> box1_off(static_cast<size_t>(J) * L, -1);
+    for (int j = 2; j < J; ++j)
+        for (int l = 0; l < L; ++l) {
+            const int sa = 1 << j, nM1 = g.PM >> j, nN1 = g.PN >> j;
+            const auto& f = fb.psi[static_cast<size_t>(j) * L + l][0];
+            double mx = 0.0;
+            for (double v : f) mx = std::max(mx, std::fabs(v));
+            std::vector<char> rsig(g.PM, 0), csig(g.PN, 0);
+            for (int kr = 0; kr < g.PM; ++kr)
+                for (int kc = 0; kc < g.PN; ++kc)
+                    if (std::fabs(f[static_cast<size_t>(kr) * g.PN + kc]) > kBoxThreshold * mx) {
+                        rsig[kr] = 1;
+                        csig[kc] = 1;
+                    }
+            if (const char* e = std::getenv("WST_BOX"))
+                if (std::atoi(e) == 0) continue;
+            box1_off[static_cast<size_t>(j) * L + l] = static_cast<int>(box.size());
+            std::vector<char> hit(sa);
+            for (int u = 0; u < nM1; ++u) {
+                for (int i = 0; i < sa; ++i) hit[i] = rsig[u + i * nM1];
+                box.push_back(cyclic_window(hit));
+            }
+            for (int v = 0; v < nN1; ++v) {
+                for (int i = 0; i < sa; ++i) hit[i] = csig[v + i * nN1];
+                box.push_back(cyclic_window(hit));
+            }
+        }
     // low-pass tap matrices in physical (digit-reversed) order, unpad + decimation folded in:
     //   GM_r[p][a] = hM_r[(s (a + 1) - perm_r(p)) mod n], s = 2^(J - r); rows padded to oms floats.
     //   Pool order: GM_0 .. GM_{J-1}, then GN_0 .. GN_{J-1} (see Blocks).
@@ -458,6 +488,7 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     if ((rc = upload(&plan->d_perm_off, t.perm_off)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_box, box)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_box_off, box_off)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_box1_off, box1_off)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_lpt, lpt)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_lpt_off, t.lpt_off)) != WST_OK) return rc;
 
@@ -476,7 +507,11 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     dp.perm = plan->d_perm; dp.perm_off = plan->d_perm_off;
     dp.o2_base = plan->d_o2;
     dp.psi2 = plan->d_psi2; dp.psi2_off = plan->d_psi2_off;
-    dp.box = plan->d_box; dp.box_off = plan->d_box_off;
+    dp.box = plan->d_box; dp.box_off = plan->d_box_off; dp.box1_off = plan->d_box1_off;
+    // the order-1 box-sparse fold pays off from s = 8 on (measured on MI355X at c2); order 2
+    // uses it for every s >= 4
+    dp.box1_min_s = 8;
+    if (const char* e = std::getenv("WST_BOX1_MIN_S")) dp.box1_min_s = std::atoi(e);
     dp.lpt = plan->d_lpt; dp.lpt_off = plan->d_lpt_off;
     // square variant (bounded FFT sizes + fused order-2 low-pass): square plane of a compiled
     // family, oM <= kLpOM and every order-2 level's column units hold ceil(oM / 2) slots
