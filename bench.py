@@ -41,6 +41,9 @@ CONFIGS = {
                C=3, M=64, N=64, J=4, L=8, batch=1024),
     "c1": dict(workload="c1: 64x64 RGB patch, J=2 L=8 order-2 (batch as given)",
                C=3, M=64, N=64, J=2, L=8, batch=1024),
+    "c5": dict(workload="c5: 64 x 256x256 4-band patches, Scattering2D J=6 L=12 order-2 (per GPU; "
+                        "384^2 and 192^2 levels HBM-staged)",
+               C=4, M=256, N=256, J=6, L=12, batch=64),
 }
 
 
@@ -212,7 +215,7 @@ def main():
     plan = _lib.Plan(M, N, J, L, 2, False)
     K, Mo, No = plan.K, plan.Mo, plan.No
     out = torch.empty((planes, 2 * K) if args.pooled else (planes, K, Mo, No), dtype=torch.float32, device=dev)
-    ws_bytes = plan.workspace_bytes(min(planes, 2048))
+    ws_bytes = plan.workspace_bytes(min(planes, plan.preferred_batch()))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -247,7 +250,7 @@ def main():
                                    ws_bytes, stream, len(slots))
         acc = [a + b for a, b in zip(acc, ms)]
     kms = dict(zip(slots, (a / args.profile_iters for a in acc)))
-    nchunks = math.ceil(planes / min(planes, 2048))
+    nchunks = math.ceil(planes / min(planes, plan.preferred_batch()))
     flops = alg_flops_per_plane(plan.PM, plan.PN, J, L)
     kms = {k: v for k, v in kms.items() if k in flops}
     dom = max(kms, key=kms.get)                     # dominant kernel of the step

@@ -70,6 +70,12 @@ int wst_padded_shape(const wst_plan* plan, int* PM, int* PN);
  * Any smaller (non-zero) workspace is accepted: the batch is then processed in chunks. */
 int wst_workspace_bytes(const wst_plan* plan, int64_t nbatch, size_t* bytes);
 
+/* Planes per workspace chunk the plan is tuned for (2048 for LDS-resident geometries; fewer for
+ * geometries with HBM-staged levels, whose workspace is tens of MB per plane).  wst_forward
+ * never processes more planes than this per chunk; size the workspace for
+ * min(nbatch, preferred) planes.  (No kymatio counterpart: sizing helper of the batched ABI.) */
+int wst_preferred_batch(const wst_plan* plan, int64_t* planes);
+
 /*
  * Scattering of `nbatch` float32 planes.
  *   d_in  : device, nbatch x M x N (or PM x PN if pre_pad), contiguous.

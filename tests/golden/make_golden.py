@@ -28,6 +28,7 @@ CASES = {
     "order1_rgb64_J3_L8": (3, 64, 64, 3, 8, 1, "max_order=1"),
     "f3_rgb128_J2_L8": (1, 128, 128, 2, 8, 2, "reference real geometry 128x128 J=2 (P=136), 1 channel"),
     "c5_ms256_J6_L12": (1, 256, 256, 6, 12, 2, "BASELINE config 5 geometry, 1 band"),
+    "staged192_gray128_J5_L8": (1, 128, 128, 5, 8, 2, "P=192: one HBM-staged level (192^2) then LDS levels"),
 }
 
 
@@ -48,6 +49,9 @@ def make(name, C, M, N, J, L, max_order):
 
 def main(names=None):
     manifest = {}
+    if names and os.path.exists(os.path.join(HERE, "manifest.json")):
+        with open(os.path.join(HERE, "manifest.json")) as f:
+            manifest = json.load(f)
     for name, (C, M, N, J, L, mo, note) in CASES.items():
         if names and name not in names:
             continue
@@ -55,9 +59,8 @@ def main(names=None):
         manifest[name] = dict(C=C, M=M, N=N, J=J, L=L, max_order=mo, out_shape=list(shape),
                               note=note, seed=0, generator="oracle/kymatio_ref.py (float64)")
         print(name, shape, flush=True)
-    if not names:
-        with open(os.path.join(HERE, "manifest.json"), "w") as f:
-            json.dump(manifest, f, indent=1)
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
 
 
 if __name__ == "__main__":

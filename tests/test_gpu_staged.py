@@ -1,0 +1,114 @@
+"""GPU tests of the HBM-staged levels (wst_staged.h): geometries whose padded planes exceed the
+LDS-resident kernels (n > 136) -- BASELINE config c5 (256x256 bands, J=6, L=12 -> 384^2 / 192^2
+staged, then 96^2 .. 12^2 in LDS) and a one-staged-level case (128^2, J=5 -> 192^2).
+
+Parity bar as everywhere (parity.TOL, per coefficient k, against the float64 oracle's goldens);
+batch / chunking / pooling / order-1 properties are checked against the golden planes placed at
+several batch positions, so the c5 oracle (~23 s per plane) is never run at test time.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import kymatio_ref as kr
+from parity import TOL, assert_parity
+
+import wst_amd  # noqa: F401
+from wst_amd import _lib
+from wst_amd.numpy import Scattering2D as NpS
+from wst_amd.torch import Scattering2D as ThS
+
+pytestmark = pytest.mark.gpu
+PHI0 = np.pi / 3.1415
+
+
+def golden(name):
+    d = load_golden(name)
+    return d, d["x_u8"].astype(np.float32) / 255
+
+
+def forward(plan, x, ws_planes=None, pooled=False):
+    B = x.shape[0]
+    shape = (B, 2 * plan.K) if pooled else (B, plan.K, plan.Mo, plan.No)
+    out = torch.empty(shape, device="cuda")
+    n = min(B, ws_planes or plan.preferred_batch())
+    ws = torch.empty(plan.workspace_bytes(n), dtype=torch.uint8, device="cuda")
+    plan.forward(x.data_ptr(), B, out.data_ptr(), pooled, ws.data_ptr(), ws.numel(),
+                 torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("name,M,J,L", [("staged192_gray128_J5_L8", 128, 5, 8),
+                                         ("c5_ms256_J6_L12", 256, 6, 12)])
+def test_staged_batch_positions_chunking_and_parity(name, M, J, L):
+    d, x = golden(name)
+    ref = d["S"][0]
+    rng = np.random.default_rng(3)
+    B = 5
+    xs = rng.integers(0, 256, (B, M, M), dtype=np.uint8).astype(np.float32) / 255
+    pos = [0, 3, 4]
+    for i in pos:
+        xs[i] = x[0]
+    plan = _lib.Plan(M, M, J, L)
+    assert plan.preferred_batch() < 2048          # staged plans bound their chunk
+    xt = torch.from_numpy(xs).cuda()
+    full = forward(plan, xt)
+    small = forward(plan, xt, ws_planes=2)        # 3 chunks: 2 + 2 + 1 planes
+    assert torch.equal(full, small), "chunked staged run differs"
+    for i in pos:
+        assert_parity(full[i].cpu().numpy()[None], ref[None], TOL, f"{name} @ {i}")
+    assert torch.isfinite(full).all()
+
+
+def test_staged_pooled_equals_pooling_of_full_output():
+    d, x = golden("staged192_gray128_J5_L8")
+    xt = torch.from_numpy(np.concatenate([x, x[:, ::-1].copy(), 0.5 * x], 0)).cuda()
+    plan = _lib.Plan(128, 128, 5, 8)
+    S = forward(plan, xt).double()
+    P = forward(plan, xt, pooled=True).double()
+    K = plan.K
+    scale = S.abs().amax(dim=(0, 2, 3))
+    assert torch.all((P[:, :K] - S.mean(dim=(-2, -1))).abs() <= 1e-6 * scale)
+    assert torch.all((P[:, K:] - S.std(dim=(-2, -1), unbiased=False)).abs() <= 1e-6 * scale)
+
+
+def test_staged_order1_against_oracle():
+    x = np.random.default_rng(4).integers(0, 256, (2, 128, 128), dtype=np.uint8).astype(np.float32) / 255
+    ref = kr.Scattering2D(J=5, shape=(128, 128), L=4, max_order=1)(x)
+    got = NpS(J=5, shape=(128, 128), L=4, max_order=1)(x)
+    assert got.shape == ref.shape == (2, 1 + 5 * 4, 4, 4)
+    assert_parity(got, ref, TOL, "staged order 1")
+
+
+def test_c5_full_size_properties():
+    """BASELINE config 5 at its stated size (64 patches x 4 bands = 256 planes of 256^2, J=6,
+    L=12): size-independent properties over the whole batch (S0 affine; S1/S2 shift-invariant
+    and positively homogeneous) + golden parity of the planes carrying the golden input."""
+    d, x = golden("c5_ms256_J6_L12")
+    rng = np.random.default_rng(12)
+    xb = rng.integers(0, 256, (64, 4, 256, 256), dtype=np.uint8).astype(np.float32) / 255
+    xb[7, 2] = x[0]
+    xb[63, 3] = x[0]
+    s = ThS(J=6, shape=(256, 256), L=12)
+    xt = torch.from_numpy(xb).cuda()
+    S = s(xt)
+    assert tuple(S.shape) == (64, 4, 2233, 4, 4)
+    assert torch.isfinite(S).all()
+    for i, c in [(7, 2), (63, 3)]:
+        assert_parity(S[i, c].cpu().numpy()[None], d["S"], TOL, f"c5 golden @ ({i},{c})")
+    a, b = 0.5, 0.25
+    S2 = s(a * xt + b)
+    d0 = (S2[:, :, 0] - (a * S[:, :, 0] + PHI0 * b)).abs().max().item()
+    assert d0 <= TOL * S2[:, :, 0].abs().max().item()
+    Sd, S2d = S.double(), S2.double()
+    scale = (a * Sd[:, :, 1:]).abs().amax(dim=(0, 1, 3, 4))
+    err = ((S2d[:, :, 1:] - a * Sd[:, :, 1:]).abs().amax(dim=(0, 1, 3, 4)) / scale).max().item()
+    assert err <= 2 * TOL, err
+
+
+def test_large_rectangular_plane_is_unsupported():
+    with pytest.raises(_lib.WSTError) as e:
+        _lib.Plan(256, 128, 4, 8)                  # 288 x 160 padded: staged needs square
+    assert e.value.code == _lib.WST_ERR_UNSUPPORTED

@@ -21,7 +21,8 @@ ABI_VERSION = 1
 # every symbol include/wst_hip.h declares
 EXPORTS = (
     "wst_abi_version", "wst_last_error", "wst_plan_create", "wst_plan_destroy",
-    "wst_output_shape", "wst_padded_shape", "wst_workspace_bytes", "wst_forward",
+    "wst_output_shape", "wst_padded_shape", "wst_workspace_bytes", "wst_preferred_batch",
+    "wst_forward",
     "wst_forward_profiled", "wst_host_filter", "wst_host_fft_lines",
 )
 
@@ -66,6 +67,8 @@ def load() -> ctypes.CDLL:
         lib.wst_padded_shape.argtypes = [c_vp] + [ctypes.POINTER(c_int)] * 2
         lib.wst_workspace_bytes.restype = c_int
         lib.wst_workspace_bytes.argtypes = [c_vp, c_i64, ctypes.POINTER(c_sz)]
+        lib.wst_preferred_batch.restype = c_int
+        lib.wst_preferred_batch.argtypes = [c_vp, ctypes.POINTER(c_i64)]
         lib.wst_forward.restype = c_int
         lib.wst_forward.argtypes = [c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_sz, c_vp]
         lib.wst_forward_profiled.restype = c_int
@@ -135,6 +138,12 @@ class Plan:
     def workspace_bytes(self, nbatch: int) -> int:
         b = ctypes.c_size_t()
         check(load().wst_workspace_bytes(self._h, int(nbatch), ctypes.byref(b)))
+        return b.value
+
+    def preferred_batch(self) -> int:
+        """Planes per workspace chunk (wst_preferred_batch)."""
+        b = ctypes.c_int64()
+        check(load().wst_preferred_batch(self._h, ctypes.byref(b)))
         return b.value
 
     def forward(self, d_in: int, nbatch: int, d_out: int, pooled: bool, d_ws: int, ws_bytes: int,

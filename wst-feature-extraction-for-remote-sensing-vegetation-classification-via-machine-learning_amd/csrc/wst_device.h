@@ -814,10 +814,13 @@ __global__ void __launch_bounds__(1024) k_o1(DevParams p, LdsLayout lay, int j1,
 // ------------------------------------------------------------------------------------------
 // k_o2: one workgroup per (plane, theta1) at fixed j1 -- all order-2 paths from U1hat
 // ------------------------------------------------------------------------------------------
-template <int FM, int FN, int MAXN, int SQ>
+// HG = 1: the level-j1 spectrum is a big (HBM-staged, wst_staged.h) level: `hexp` holds the
+// fully transformed half spectra in natural order, the fold reads them from HBM (no LDS copy,
+// no column FFT) and the paths start at j2first (the first LDS-resident level).
+template <int FM, int FN, int MAXN, int SQ, int HG = 0>
 __global__ void __launch_bounds__(1024) k_o2(DevParams p, LdsLayout lay, int j1, int nimg,
                                              long long img0, const float2* __restrict__ hexp,
-                                             float* __restrict__ out, int pooled) {
+                                             float* __restrict__ out, int pooled, int j2first) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int J = p.J, L = p.L;
     const int item = xcd_item(nimg * L);
@@ -827,25 +830,31 @@ __global__ void __launch_bounds__(1024) k_o2(DevParams p, LdsLayout lay, int j1,
     const int PM = p.PM, PN = p.PN;
     const int nM1 = PM >> j1, nN1 = PN >> j1, n1 = nM1 * nN1;
     const int hld = (nN1 >> 1) + 1;
-    float2* H = reinterpret_cast<float2*>(smem);
+    const float2* Hg = hexp + static_cast<long long>(item) * nM1 * hld;
+    const float2* H = HG ? Hg : reinterpret_cast<const float2*>(smem);
     float2* B = reinterpret_cast<float2*>(smem + lay.off_b);
     float* S = reinterpret_cast<float*>(smem + lay.off_s);
     const Tables tb = load_tables(p, lay, smem);
     const int dbg = p.dbg_skip;
-
-    // 1. half spectrum rows -> LDS, then the column FFTs (rows digit-reversed -> natural)
-    const float2* Hg = hexp + static_cast<long long>(item) * nM1 * hld;
-    for (int o = threadIdx.x; o < nM1 * hld; o += blockDim.x) H[o] = Hg[o];
-    __syncthreads();
     wstfft::EpiIdentity id;
-    if (!(dbg & 4))
-        lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(H, wstfft::Lines{1, 0, hld, 1, hld},
-                                                                     nM1, tb.twM(j1), id);
+    // order-2 path sizes: <= MAXN / 2 below an LDS-resident level of class MAXN, <= MAXN after a
+    // big level
+    constexpr int PHI = (SQ && !HG) ? MAXN / 2 : MAXN;
+
+    if constexpr (!HG) {
+        // 1. half spectrum rows -> LDS, then the column FFTs (rows digit-reversed -> natural)
+        float2* Hl = reinterpret_cast<float2*>(smem);
+        for (int o = threadIdx.x; o < nM1 * hld; o += blockDim.x) Hl[o] = Hg[o];
+        __syncthreads();
+        if (!(dbg & 4))
+            lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(
+                Hl, wstfft::Lines{1, 0, hld, 1, hld}, nM1, tb.twM(j1), id);
+    }
 
     // 2. order-2 paths in batches: Hermitian fold -> |ifft| -> S2 low-pass
     const int kbase = p.o2_base[j1 * L + l1];
     const int nq = (L + 1) >> 1;
-    for (int j2 = j1 + 1; j2 < J; ++j2) {
+    for (int j2 = j2first; j2 < J; ++j2) {
         const int nM2 = PM >> j2, nN2 = PN >> j2, ld2 = odd_ld(nN2);
         const int pslot = nM2 * ld2;
         const int s2 = 1 << (j2 - j1);
@@ -865,10 +874,10 @@ __global__ void __launch_bounds__(1024) k_o2(DevParams p, LdsLayout lay, int j1,
             if constexpr (SQ) {
                 // rows, then the column pass fused with |.| and the S2 low-pass
                 if (!(dbg & 16))
-                    lds_fft_lines<FN, 0, MAXN / 2, kDR, true>(
+                    lds_fft_lines<FN, 0, PHI, kDR, true>(
                         B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, nN2, tb.twN(j2), id);
                 if (!(dbg & 64))
-                    family_cols_modlp<FM, 0, MAXN / 2>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
+                    family_cols_modlp<FM, 0, PHI>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
                                                        tb.gM(j2), tb.gN(j2), lay.oms, p.oM, p.oN,
                                                        scale2, S);
                 emit(S, npath, kbase + (j2 - j1 - 1) * L + l2a, img, p.K, p.oM, p.oN, out, pooled);

@@ -56,7 +56,14 @@ int odd_part(int n) {
 int family_of(int P) {
     const int o = odd_part(P);
     const bool compiled = (o == 1 || o == 3 || o == 5 || o == 9 || o == 17);
-    return (compiled && P <= wstfft::kMaxFamilyN) ? o : 0;
+    return compiled ? o : 0;
+}
+const wstlaunch::BigOps* big_ops(int n) {
+#define WST_BIG_OPS(N) \
+    if (n == N) return &wstlaunch::WST_BIG_GETTER(N)();
+    WST_BIG_SIZES(WST_BIG_OPS)
+#undef WST_BIG_OPS
+    return nullptr;
 }
 const FamilyOps* family_ops(int fm, int fn) {
 #define WST_PAIR_OPS(A, B) \
@@ -66,6 +73,7 @@ const FamilyOps* family_ops(int fm, int fn) {
     return nullptr;
 }
 int cap_for(int n) { return n <= 12 ? 12 : n <= 24 ? 24 : n <= 48 ? 48 : 136; }
+constexpr int kBigRows = 8;   // rows per row-pass workgroup of the staged levels
 
 size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
@@ -110,6 +118,8 @@ struct wst_plan {
     int* d_box = nullptr;
     int* d_box_off = nullptr;
     int* d_box1_off = nullptr;
+    std::vector<long long> psi2_off_host;
+    std::vector<int> box_off_host;
     float* d_lpt = nullptr;
     int* d_lpt_off = nullptr;
     // launch geometry
@@ -122,6 +132,19 @@ struct wst_plan {
     std::vector<int> o1_threads, o2_threads, cap;
     std::vector<size_t> o1_lds, o2_lds;
     std::vector<LdsLayout> o1_lay, o2_lay;
+    // HBM-staged leading levels (n > kBigMinN): wst_staged.h
+    int rb = 0;
+    int oms = 4;                                  // tap-matrix row stride
+    std::vector<const wstlaunch::BigOps*> big;    // per staged level
+    std::vector<int> lpn_off;                     // natural tap matrices: [2r] GM_r, [2r+1] GN_r
+    float* d_lpn = nullptr;
+    std::vector<LdsLayout> hg_lay;                // k_o2 (global spectrum) after a staged j1
+    std::vector<size_t> hg_lds;
+    std::vector<int> hg_threads, hg_j2first;
+    size_t big_rows_lds = 0, big_cols_lds = 0;
+    std::vector<size_t> ws_hbig;                  // U1hat half spectra of staged j1 (per plane)
+    size_t ws_tmp = 0, ws_ureal = 0, ws_part = 0, ws_csum = 0, ws_mean = 0;
+    int64_t max_chunk = 2048;                     // planes per workspace chunk
     // workspace per plane: Xhat, then the half spectra of every j1 < J-1
     size_t ws_xhat = 0;
     std::vector<size_t> ws_h_off;   // byte offset of level j1's half spectra (per plane units)
@@ -152,6 +175,7 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_box1_off);
     (void)hipFree(p->d_lpt);
     (void)hipFree(p->d_lpt_off);
+    (void)hipFree(p->d_lpn);
     if (p->ws) (void)hipFree(p->ws);
     delete p;
 }
@@ -449,6 +473,21 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
             t.lpt_len[2 * r + d] = n * oms;
         }
     t.lpt_off.back() = static_cast<int>(lpt.size());
+    // the same tap matrices in natural order (HBM-staged levels use natural-order transforms)
+    std::vector<float> lpn;
+    plan->lpn_off.assign(2 * static_cast<size_t>(J), 0);
+    for (int r = 0; r < J; ++r)
+        for (int d = 0; d < 2; ++d) {
+            const int n = (d == 0 ? g.PM : g.PN) >> r;
+            const int no = d == 0 ? g.oM : g.oN;
+            const int sdec = 1 << (J - r);
+            const auto& h = d == 0 ? fb.hM[r] : fb.hN[r];
+            plan->lpn_off[2 * r + d] = static_cast<int>(lpn.size());
+            for (int p = 0; p < n; ++p)
+                for (int a = 0; a < oms; ++a)
+                    lpn.push_back(a < no ? static_cast<float>(h[((sdec * (a + 1) - p) % n + n) % n]) : 0.f);
+        }
+    plan->oms = oms;
     // twiddles exp(-2 pi i k / n) per level and side; pool order: M levels 0..J, then N levels
     std::vector<float2> tw;
     t.tw_off.assign(2 * static_cast<size_t>(J + 1) + 1, 0);
@@ -489,8 +528,11 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     if ((rc = upload(&plan->d_box, box)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_box_off, box_off)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_box1_off, box1_off)) != WST_OK) return rc;
+    plan->psi2_off_host = psi2_off;
+    plan->box_off_host = box_off;
     if ((rc = upload(&plan->d_lpt, lpt)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_lpt_off, t.lpt_off)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_lpn, lpn)) != WST_OK) return rc;
 
     DevParams& dp = plan->dp;
     dp.M = g.M; dp.N = g.N; dp.PM = g.PM; dp.PN = g.PN; dp.J = J; dp.L = L;
@@ -529,11 +571,29 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
                         std::to_string(g.PN) + " padded plane at level " + std::to_string(j) +
                         " exceeds the LDS-resident path (160 KiB per CU)");
     };
-    plan->prep_lds = layout(plan->prep_lay, static_cast<size_t>(g.PM) * odd_ld(g.PN) * sizeof(float2),
-                            0, t, Blocks{0, 0, true}, 0, 0, omn);
-    plan->prep_lay.npm = 0;   // k_prep works in natural order
-    if (plan->prep_lds > static_cast<size_t>(kMaxLds)) return too_big("k_prep", 0);
-    plan->prep_threads = static_cast<size_t>(g.PM) * g.PN >= 4096 ? 512 : 256;
+    // leading levels too large for the LDS-resident kernels run HBM-staged (wst_staged.h)
+    while (plan->rb < J && std::max(g.PM, g.PN) >> plan->rb > wstbig::kBigMinN) ++plan->rb;
+    if (plan->rb > 0) {
+        if (g.PM != g.PN || !plan->sq)
+            return fail(WST_ERR_UNSUPPORTED,
+                        "padded plane " + std::to_string(g.PM) + "x" + std::to_string(g.PN) +
+                            " needs HBM-staged levels, implemented for square planes of a compiled "
+                            "FFT family with M / 2^J <= 8 only");
+        plan->big.assign(plan->rb, nullptr);
+        for (int r = 0; r < plan->rb; ++r)
+            if (!(plan->big[r] = big_ops(g.PM >> r)))
+                return fail(WST_ERR_UNSUPPORTED, "no HBM-staged FFT compiled for level size " +
+                                                     std::to_string(g.PM >> r));
+        const int nmax = g.PM;
+        plan->big_rows_lds = (nmax + 2 * kBigRows * (nmax | 1)) * sizeof(float2);
+        plan->big_cols_lds = (nmax + wstbig::kColTile * (nmax | 1)) * sizeof(float2);
+    } else {
+        plan->prep_lds = layout(plan->prep_lay, static_cast<size_t>(g.PM) * odd_ld(g.PN) * sizeof(float2),
+                                0, t, Blocks{0, 0, true}, 0, 0, omn);
+        plan->prep_lay.npm = 0;   // k_prep works in natural order
+        if (plan->prep_lds > static_cast<size_t>(kMaxLds)) return too_big("k_prep", 0);
+        plan->prep_threads = static_cast<size_t>(g.PM) * g.PN >= 4096 ? 512 : 256;
+    }
 
     plan->o1_threads.assign(J, 64);
     plan->o2_threads.assign(J, 64);
@@ -545,7 +605,55 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     plan->ws_h_off.assign(J, 0);
     plan->ws_xhat = static_cast<size_t>(g.PM) * g.PN * sizeof(float2);
     size_t wsp = plan->ws_xhat;
-    for (int j1 = 0; j1 < J; ++j1) {
+    auto pslot = [&](int j) { return static_cast<size_t>(g.PM >> j) * odd_ld(g.PN >> j); };
+    plan->ws_hbig.assign(J, 0);
+    plan->hg_lay.assign(J, LdsLayout{});
+    plan->hg_lds.assign(J, 0);
+    plan->hg_threads.assign(J, 64);
+    plan->hg_j2first.assign(J, J);
+    size_t tmp_c = 0, part_n = static_cast<size_t>(g.PM);
+    for (int j1 = 0; j1 < plan->rb; ++j1) {
+        // staged order 1 (+ U1hat for order 2); order-2 paths staged while j2 < rb, then k_o2 HG
+        const size_t n1 = static_cast<size_t>(g.PM >> j1);
+        const bool do2 = max_order >= 2 && j1 < J - 1;
+        tmp_c = std::max(tmp_c, static_cast<size_t>(L) * n1 * n1);
+        part_n = std::max(part_n, static_cast<size_t>(L) * n1);
+        if (!do2) continue;
+        plan->ws_hbig[j1] = wsp;
+        wsp += align16(static_cast<size_t>(L) * n1 * (n1 / 2 + 1) * sizeof(float2));
+        plan->ws_ureal = std::max(plan->ws_ureal, static_cast<size_t>(L) * n1 * n1 * sizeof(float));
+        for (int j2 = j1 + 1; j2 < plan->rb; ++j2) {
+            const size_t n2 = static_cast<size_t>(g.PM >> j2);
+            tmp_c = std::max(tmp_c, static_cast<size_t>(L) * n2 * n2);
+            part_n = std::max(part_n, static_cast<size_t>(L) * n2);
+        }
+        const int j2f = std::max(j1 + 1, plan->rb);
+        plan->hg_j2first[j1] = j2f;
+        if (j2f >= J) continue;
+        // two paths of the first resident level (the smaller levels batch as many as fit)
+        const size_t bcap = 2 * pslot(j2f);
+        size_t smax = 0;
+        for (int j2 = j2f; j2 < J; ++j2)
+            smax = std::max(smax, static_cast<size_t>(paths_per_batch(bcap, pslot(j2), L)) * omn);
+        plan->hg_lds[j1] = layout(plan->hg_lay[j1], 0, bcap * sizeof(float2), t, Blocks{j2f, J - 1, false},
+                                  1, 0, smax, Blocks{j2f, J - 1, false}, oms);
+        plan->hg_threads[j1] = default_threads(static_cast<size_t>(g.PM >> j2f) * (g.PN >> j2f));
+        if (plan->hg_lds[j1] > static_cast<size_t>(kMaxLds)) return too_big("k_o2 (global spectrum)", j1);
+    }
+    if (plan->rb > 0) {
+        plan->ws_tmp = wsp;
+        wsp += align16(tmp_c * sizeof(float2));
+        const size_t ureal_bytes = plan->ws_ureal;
+        plan->ws_ureal = wsp;
+        wsp += align16(ureal_bytes);
+        plan->ws_part = wsp;
+        wsp += align16(part_n * oms * sizeof(float));
+        plan->ws_csum = wsp;
+        wsp += align16(part_n * sizeof(float));
+        plan->ws_mean = wsp;
+        wsp += align16((1 + static_cast<size_t>(L)) * sizeof(float));
+    }
+    for (int j1 = plan->rb; j1 < J; ++j1) {
         const int nM1 = g.PM >> j1, nN1 = g.PN >> j1;
         const size_t n1 = static_cast<size_t>(nM1) * nN1;
         const bool do2 = max_order >= 2 && j1 < J - 1;
@@ -562,7 +670,6 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
         plan->ws_h_off[j1] = wsp;
         wsp += static_cast<size_t>(L) * nM1 * hld * sizeof(float2);
         // B holds two paths of level j1+1 or all L paths of level j1+2, whichever is larger
-        auto pslot = [&](int j) { return static_cast<size_t>(g.PM >> j) * odd_ld(g.PN >> j); };
         size_t bcap = 2 * pslot(j1 + 1);
         if (j1 + 2 < J) bcap = std::max(bcap, static_cast<size_t>(L) * pslot(j1 + 2));
         size_t smax = 0;
@@ -579,6 +686,8 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
         if (plan->o2_lds[j1] > static_cast<size_t>(kMaxLds)) return too_big("k_o2", j1);
     }
     plan->ws_plane = align16(wsp);
+    if (plan->rb > 0)   // staged plans hold ~tens of MB per plane: bound the chunk to ~2 GB
+        plan->max_chunk = std::max<int64_t>(1, std::min<int64_t>(2048, (size_t(2) << 30) / plan->ws_plane));
     if (std::getenv("WST_VERBOSE")) {
         std::fprintf(stderr, "[wst] plan %dx%d J=%d L=%d P=%dx%d fam=(%d,%d) sq=%d prep_lds=%zu\n", M, N, J, L,
                      g.PM, g.PN, plan->fam_m, plan->fam_n, plan->sq, plan->prep_lds);
@@ -590,6 +699,10 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     threads_override("WST_O1_THREADS", plan->o1_threads);
     threads_override("WST_O2_THREADS", plan->o2_threads);
     WST_HIP_CHECK(plan->ops->set_attrs());
+    if (plan->rb > 0) {
+        WST_HIP_CHECK(wstlaunch::wst_big_common_ops().set_attrs());
+        for (int r = 0; r < plan->rb; ++r) WST_HIP_CHECK(plan->big[r]->set_attrs());
+    }
 
     *out = plan.release();
     g_last_error.clear();
@@ -620,6 +733,12 @@ int wst_workspace_bytes(const wst_plan* plan, int64_t nbatch, size_t* bytes) {
     if (!plan || !bytes) return fail(WST_ERR_INVALID, "plan/bytes is NULL");
     if (nbatch < 0) return fail(WST_ERR_INVALID, "nbatch < 0");
     *bytes = static_cast<size_t>(nbatch) * plan->ws_plane;
+    return WST_OK;
+}
+
+int wst_preferred_batch(const wst_plan* plan, int64_t* planes) {
+    if (!plan || !planes) return fail(WST_ERR_INVALID, "plan/planes is NULL");
+    *planes = plan->max_chunk;
     return WST_OK;
 }
 
@@ -661,6 +780,162 @@ struct LaunchTimer {
     }
 };
 
+// One LDS-resident level j1: k_o1 (S1 + U1 half-spectrum export), then k_o2 (every S2 of j1).
+int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsigned char* base,
+                   int64_t chunk, const float2* xhat, float* d_out, int pooled, hipStream_t stream,
+                   LaunchTimer& timer) {
+    const wst::Geometry& g = plan->g;
+    const bool do2 = g.max_order >= 2 && j1 < g.J - 1;
+    float2* hexp = do2 ? reinterpret_cast<float2*>(base + plan->ws_h_off[j1] * chunk) : nullptr;
+    int rc;
+    if ((rc = timer.begin(stream)) != WST_OK) return rc;
+    plan->ops->o1(plan->cap[j1], plan->sq,
+                  Launch{dim3(nimg * g.L), dim3(plan->o1_threads[j1]), plan->o1_lds[j1], stream},
+                  plan->dp, plan->o1_lay[j1], j1, nimg, img0, xhat, hexp, d_out, pooled);
+    WST_HIP_CHECK(hipGetLastError());
+    if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
+    if (!do2) return WST_OK;
+    if ((rc = timer.begin(stream)) != WST_OK) return rc;
+    plan->ops->o2(plan->cap[j1], plan->sq, 0,
+                  Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
+                  plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j1 + 1);
+    WST_HIP_CHECK(hipGetLastError());
+    return timer.end(stream, 1 + g.J + j1);
+}
+
+// The HBM-staged levels r < rb of one chunk (wst_staged.h): S0 + Xhat, then per staged j1 the
+// order-1 path (S1, U1hat) and its order-2 paths (staged while j2 < rb, then k_o2 on the global
+// spectrum).  Timing slots as the resident kernels: prep, o1 at j1, o2 at j1.
+int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img0,
+                  unsigned char* base, int64_t chunk, float* d_out, int pooled, hipStream_t stream,
+                  LaunchTimer& timer) {
+    using namespace wstbig;
+    const wst::Geometry& g = plan->g;
+    const DevParams& dp = plan->dp;
+    const int J = g.J, L = g.L, PM = g.PM, nq = (L + 1) / 2;
+    const auto& cm = wstlaunch::wst_big_common_ops();
+    float2* xhat = reinterpret_cast<float2*>(base);
+    float2* tmp = reinterpret_cast<float2*>(base + plan->ws_tmp * chunk);
+    float* ureal = reinterpret_cast<float*>(base + plan->ws_ureal * chunk);
+    float* part = reinterpret_cast<float*>(base + plan->ws_part * chunk);
+    float* csum = reinterpret_cast<float*>(base + plan->ws_csum * chunk);
+    float* mean = reinterpret_cast<float*>(base + plan->ws_mean * chunk);   // [plane] then [plane*L + l1]
+    float* umean = mean + nimg;
+    const dim3 tb(kBigThreads);
+    auto gnat = [&](int r, int d) { return plan->d_lpn + plan->lpn_off[2 * r + d]; };
+    auto args = [&](int mode, int r) {
+        BigArgs a{};
+        a.mode = mode;
+        a.n = PM >> r;
+        a.lvl = r;
+        a.rows = kBigRows;
+        a.ncols = PM >> r;
+        a.L = L;
+        a.img0 = img0;
+        a.oms = plan->oms;
+        return a;
+    };
+    int rc;
+    // ---- S0 and Xhat (level 0) ----
+    if ((rc = timer.begin(stream)) != WST_OK) return rc;
+    cm.mean(Launch{dim3(nimg), tb, 0, stream}, dp, in, mean);
+    {
+        BigArgs a = args(kRowPad, 0);
+        a.in = in;
+        a.mean = mean;
+        a.tpart = part;
+        a.gnat = gnat(0, 1);
+        a.dst = xhat;
+        plan->big[0]->rows(false, Launch{dim3(PM / kBigRows, nimg), tb, plan->big_rows_lds, stream}, dp, a);
+        BigArgs c = args(kColStore, 0);
+        c.dst = xhat;
+        plan->big[0]->cols(false, Launch{dim3((PM + kColTile - 1) / kColTile, nimg), tb, plan->big_cols_lds, stream},
+                           dp, c);
+        cm.final_(Launch{dim3(nimg), dim3(64), 0, stream}, dp, kFinalRows, 0, PM, plan->oms, part,
+                  gnat(0, 0), nullptr, nullptr, L, 0, 0, 0, 1, img0, d_out, pooled);
+    }
+    WST_HIP_CHECK(hipGetLastError());
+    if ((rc = timer.end(stream, 0)) != WST_OK) return rc;
+
+    for (int j1 = 0; j1 < plan->rb; ++j1) {
+        const int n1 = PM >> j1, hld = n1 / 2 + 1;
+        const bool do2 = g.max_order >= 2 && j1 < J - 1;
+        const auto* B1 = plan->big[j1];
+        float2* hbig = do2 ? reinterpret_cast<float2*>(base + plan->ws_hbig[j1] * chunk) : nullptr;
+        // ---- order 1: fold + inverse rows, inverse columns + |.| + low-pass partials, S1 ----
+        if ((rc = timer.begin(stream)) != WST_OK) return rc;
+        BigArgs a = args(kRowFold1, j1);
+        a.xhat = xhat;
+        a.j1 = j1;
+        a.dst = tmp;
+        B1->rows(true, Launch{dim3(n1 / kBigRows, nimg * L), tb, plan->big_rows_lds, stream}, dp, a);
+        BigArgs c = args(kColModLp, j1);
+        c.dst = tmp;
+        c.uout = do2 ? ureal : nullptr;
+        c.vpart = part;
+        c.csum = csum;
+        c.scale = 1.f / (static_cast<float>(g.PM) * static_cast<float>(g.PN));
+        c.gnat = gnat(j1, 0);
+        B1->cols(true, Launch{dim3((n1 + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds, stream},
+                 dp, c);
+        cm.final_(Launch{dim3(nimg * L), dim3(64), 0, stream}, dp, kFinalCols, 1, n1, plan->oms, part,
+                  gnat(j1, 1), csum, do2 ? umean : nullptr, L, j1, 0, 0, 1, img0, d_out, pooled);
+        if (do2) {
+            // U1hat = fft2(U1 - mean) as half spectra (natural order) for the order-2 folds
+            BigArgs r2 = args(kRowReal2, j1);
+            r2.ureal = ureal;
+            r2.mean = umean;
+            r2.dst = hbig;
+            B1->rows(false, Launch{dim3(n1 / kBigRows, nimg * L), tb, plan->big_rows_lds, stream}, dp, r2);
+            BigArgs c2 = args(kColStore, j1);
+            c2.ncols = hld;
+            c2.dst = hbig;
+            B1->cols(false, Launch{dim3((hld + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds, stream},
+                     dp, c2);
+        }
+        WST_HIP_CHECK(hipGetLastError());
+        if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
+        if (!do2) continue;
+        // ---- order 2 from the staged U1hat ----
+        if ((rc = timer.begin(stream)) != WST_OK) return rc;
+        for (int j2 = j1 + 1; j2 < plan->rb; ++j2) {
+            const int n2 = PM >> j2;
+            const auto* B2 = plan->big[j2];
+            for (int l1 = 0; l1 < L; ++l1) {
+                BigArgs f = args(kRowFold2, j2);
+                f.hsrc = hbig;
+                f.n1 = n1;
+                f.l1 = l1;
+                f.j2 = j2;
+                f.psi2 = dp.psi2 + plan->psi2_off_host[(static_cast<size_t>(j2) * J + j1) * nq];
+                f.pstride = static_cast<long long>(n1) * n1;
+                f.box = plan->d_box + plan->box_off_host[static_cast<size_t>(j2) * J + j1];
+                f.npair = nq;
+                f.npath = L;
+                f.dst = tmp;
+                B2->rows(true, Launch{dim3(n2 / kBigRows, nimg * nq), tb, plan->big_rows_lds, stream}, dp, f);
+                BigArgs m2 = args(kColModLp, j2);
+                m2.dst = tmp;
+                m2.vpart = part;
+                m2.csum = csum;
+                m2.scale = 1.f / (static_cast<float>(n1) * static_cast<float>(n1));
+                m2.gnat = gnat(j2, 0);
+                B2->cols(true, Launch{dim3((n2 + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds, stream},
+                         dp, m2);
+                cm.final_(Launch{dim3(nimg * L), dim3(64), 0, stream}, dp, kFinalCols, 2, n2, plan->oms,
+                          part, gnat(j2, 1), nullptr, nullptr, L, j1, l1, j2, L, img0, d_out, pooled);
+            }
+        }
+        const int j2f = plan->hg_j2first[j1];
+        if (j2f < J)
+            plan->ops->o2(136, 1, 1, Launch{dim3(nimg * L), dim3(plan->hg_threads[j1]), plan->hg_lds[j1], stream},
+                          dp, plan->hg_lay[j1], j1, nimg, img0, hbig, d_out, pooled, j2f);
+        WST_HIP_CHECK(hipGetLastError());
+        if ((rc = timer.end(stream, 1 + J + j1)) != WST_OK) return rc;
+    }
+    return WST_OK;
+}
+
 // Timing slots of wst_forward_profiled: [0] k_prep, [1 + j1] k_o1 at j1, [1 + J + j1] k_o2 at j1.
 int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float* d_out, int pooled,
                  void* d_workspace, size_t workspace_bytes, void* stream_, float* kms, int nkms) {
@@ -679,8 +954,8 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
     void* ws = d_workspace;
     size_t wsb = workspace_bytes;
     if (!ws) {
-        // internal workspace: up to 2048 planes per chunk
-        const int64_t want = std::min<int64_t>(nbatch, 2048);
+        // internal workspace: up to max_chunk planes per chunk
+        const int64_t want = std::min<int64_t>(nbatch, plan->max_chunk);
         std::lock_guard<std::mutex> lk(plan->ws_mu);
         if (plan->ws_bytes < want * plane_ws) {
             if (plan->ws) {
@@ -695,7 +970,7 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
         ws = plan->ws;
         wsb = plan->ws_bytes;
     }
-    const int64_t chunk = static_cast<int64_t>(wsb / plane_ws);
+    const int64_t chunk = std::min<int64_t>(static_cast<int64_t>(wsb / plane_ws), plan->max_chunk);
     if (chunk < 1) return fail(WST_ERR_INVALID, "workspace smaller than one plane's share");
     const int inM = plan->dp.pre_pad ? g.PM : g.M, inN = plan->dp.pre_pad ? g.PN : g.N;
     // workspace regions (chunk-sized): Xhat, then each level's half spectra
@@ -707,28 +982,25 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
     for (int64_t c0 = 0; c0 < nbatch; c0 += chunk) {
         const int nimg = static_cast<int>(std::min<int64_t>(chunk, nbatch - c0));
         const long long img0 = static_cast<long long>(c0);
+        if (plan->rb > 0) {
+            if ((rc = staged_levels(plan, d_in + c0 * inM * inN, nimg, img0, base, chunk, d_out, pooled,
+                                    stream, timer)) != WST_OK)
+                return rc;
+            for (int j1 = plan->rb; j1 < g.J; ++j1)
+                if ((rc = resident_level(plan, j1, nimg, img0, base, chunk, xhat, d_out, pooled, stream,
+                                         timer)) != WST_OK)
+                    return rc;
+            continue;
+        }
         if ((rc = timer.begin(stream)) != WST_OK) return rc;
         plan->ops->prep(Launch{dim3(nimg), dim3(plan->prep_threads), plan->prep_lds, stream},
                         plan->dp, plan->prep_lay, d_in + c0 * inM * inN, img0, xhat, d_out, pooled);
         WST_HIP_CHECK(hipGetLastError());
         if ((rc = timer.end(stream, 0)) != WST_OK) return rc;
-        for (int j1 = 0; j1 < g.J; ++j1) {
-            const bool do2 = g.max_order >= 2 && j1 < g.J - 1;
-            float2* hexp = do2 ? reinterpret_cast<float2*>(base + plan->ws_h_off[j1] * chunk) : nullptr;
-            if ((rc = timer.begin(stream)) != WST_OK) return rc;
-            plan->ops->o1(plan->cap[j1], plan->sq,
-                          Launch{dim3(nimg * g.L), dim3(plan->o1_threads[j1]), plan->o1_lds[j1], stream},
-                          plan->dp, plan->o1_lay[j1], j1, nimg, img0, xhat, hexp, d_out, pooled);
-            WST_HIP_CHECK(hipGetLastError());
-            if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
-            if (!do2) continue;
-            if ((rc = timer.begin(stream)) != WST_OK) return rc;
-            plan->ops->o2(plan->cap[j1], plan->sq,
-                          Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
-                          plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled);
-            WST_HIP_CHECK(hipGetLastError());
-            if ((rc = timer.end(stream, 1 + g.J + j1)) != WST_OK) return rc;
-        }
+        for (int j1 = 0; j1 < g.J; ++j1)
+            if ((rc = resident_level(plan, j1, nimg, img0, base, chunk, xhat, d_out, pooled, stream,
+                                     timer)) != WST_OK)
+                return rc;
     }
     return WST_OK;
 }

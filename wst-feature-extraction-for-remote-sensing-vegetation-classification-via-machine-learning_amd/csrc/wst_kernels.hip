@@ -1,6 +1,7 @@
 // Kernel instantiations of one FFT size-family pair (WST_FAM_M, WST_FAM_N), set by the Makefile:
 // k_prep, and k_o1 / k_o2 per size class (caps 12/24/48/136), generic and -- for square families
-// -- the bounded, fused-low-pass variant (wst_device.h).
+// -- the bounded, fused-low-pass variant and the global-spectrum k_o2 after a big level
+// (wst_device.h).
 #include "wst_launch.h"
 
 #ifndef WST_FAM_M
@@ -18,7 +19,7 @@ hipError_t attrs_cap() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o1<FM, FN, C, SQ>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds);
     if (e != hipSuccess) return e;
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2<FM, FN, C, SQ>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2<FM, FN, C, SQ, 0>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds);
 }
 
@@ -36,7 +37,11 @@ hipError_t set_attrs() {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds);
     if (e != hipSuccess) return e;
     if ((e = attrs_all<0>()) != hipSuccess) return e;
-    if constexpr (kSquareFamily) return attrs_all<1>();
+    if constexpr (kSquareFamily) {
+        if ((e = attrs_all<1>()) != hipSuccess) return e;
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2<FM, FN, 136, 1, 1>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds);
+    }
     return hipSuccess;
 }
 
@@ -59,16 +64,20 @@ void o1_sq(int cap, const Launch& q, const DevParams& dp, const LdsLayout& lay, 
 #undef WST_O1_CAP
 }
 
-template <int SQ>
+template <int SQ, int HG>
 void o2_sq(int cap, const Launch& q, const DevParams& dp, const LdsLayout& lay, int j1, int nimg,
-           long long img0, const float2* hexp, float* out, int pooled) {
-#define WST_O2_CAP(C)                                                                            \
-    if (cap == C) {                                                                              \
-        hipLaunchKernelGGL((wstdev::k_o2<FM, FN, C, SQ>), q.grid, q.block, q.lds, q.st, dp, lay, \
-                           j1, nimg, img0, hexp, out, pooled);                                   \
-        return;                                                                                  \
+           long long img0, const float2* hexp, float* out, int pooled, int j2first) {
+#define WST_O2_CAP(C)                                                                              \
+    if (cap == C) {                                                                                \
+        hipLaunchKernelGGL((wstdev::k_o2<FM, FN, C, SQ, HG>), q.grid, q.block, q.lds, q.st, dp,   \
+                           lay, j1, nimg, img0, hexp, out, pooled, j2first);                       \
+        return;                                                                                    \
     }
-    WST_O2_CAP(12) WST_O2_CAP(24) WST_O2_CAP(48) WST_O2_CAP(136)
+    if constexpr (HG) {
+        WST_O2_CAP(136)
+    } else {
+        WST_O2_CAP(12) WST_O2_CAP(24) WST_O2_CAP(48) WST_O2_CAP(136)
+    }
 #undef WST_O2_CAP
 }
 
@@ -79,11 +88,13 @@ void o1(int cap, int sq, const Launch& q, const DevParams& dp, const LdsLayout& 
     o1_sq<0>(cap, q, dp, lay, j1, nimg, img0, xhat, hexp, out, pooled);
 }
 
-void o2(int cap, int sq, const Launch& q, const DevParams& dp, const LdsLayout& lay, int j1,
-        int nimg, long long img0, const float2* hexp, float* out, int pooled) {
-    if constexpr (kSquareFamily)
-        if (sq) return o2_sq<1>(cap, q, dp, lay, j1, nimg, img0, hexp, out, pooled);
-    o2_sq<0>(cap, q, dp, lay, j1, nimg, img0, hexp, out, pooled);
+void o2(int cap, int sq, int hg, const Launch& q, const DevParams& dp, const LdsLayout& lay, int j1,
+        int nimg, long long img0, const float2* hexp, float* out, int pooled, int j2first) {
+    if constexpr (kSquareFamily) {
+        if (hg) return o2_sq<1, 1>(cap, q, dp, lay, j1, nimg, img0, hexp, out, pooled, j2first);
+        if (sq) return o2_sq<1, 0>(cap, q, dp, lay, j1, nimg, img0, hexp, out, pooled, j2first);
+    }
+    o2_sq<0, 0>(cap, q, dp, lay, j1, nimg, img0, hexp, out, pooled, j2first);
 }
 
 }  // namespace

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include "wst_device.h"
+#include "wst_staged.h"
 
 namespace wstlaunch {
 
@@ -27,9 +28,33 @@ struct FamilyOps {
     // cap: size class (12/24/48/136); sq: square fused variant (only for fm == fn > 0)
     void (*o1)(int cap, int sq, const Launch&, const DevParams&, const LdsLayout&, int j1, int nimg,
                long long img0, const float2* xhat, float2* hexp, float* out, int pooled);
-    void (*o2)(int cap, int sq, const Launch&, const DevParams&, const LdsLayout&, int j1, int nimg,
-               long long img0, const float2* hexp, float* out, int pooled);
+    // hg: spectrum of a big level read from HBM (square families, cap 136), paths from j2first
+    void (*o2)(int cap, int sq, int hg, const Launch&, const DevParams&, const LdsLayout&, int j1,
+               int nimg, long long img0, const float2* hexp, float* out, int pooled, int j2first);
 };
+
+// HBM-staged passes of one big level size N (wst_staged.h), compiled per N (wst_staged.hip).
+struct BigOps {
+    int n;
+    hipError_t (*set_attrs)();
+    void (*rows)(bool inverse, const Launch&, const DevParams&, const wstbig::BigArgs&);
+    void (*cols)(bool inverse, const Launch&, const DevParams&, const wstbig::BigArgs&);
+};
+#define WST_BIG_SIZES(X) X(144) X(160) X(192) X(256) X(272) X(288) X(320) X(384) X(512)
+#define WST_BIG_GETTER(N) wst_big_ops_##N
+#define WST_DECLARE_BIG(N) const BigOps& WST_BIG_GETTER(N)();
+WST_BIG_SIZES(WST_DECLARE_BIG)
+#undef WST_DECLARE_BIG
+
+// size-independent staged kernels (k_big_mean, k_big_final), in the N = 0 object
+struct BigCommonOps {
+    hipError_t (*set_attrs)();
+    void (*mean)(const Launch&, const DevParams&, const float* in, float* mean);
+    void (*final_)(const Launch&, const DevParams&, int fmode, int kind, int n, int oms,
+                   const float* part, const float* G, const float* csum, float* mean_out, int L,
+                   int j1, int l1, int j2, int npath, long long img0, float* out, int pooled);
+};
+const BigCommonOps& wst_big_common_ops();
 
 // The compiled family pairs (rows, columns); family 0 = generic O(n) DFT.
 #define WST_FAMILY_PAIRS(X) X(0, 0) X(1, 1) X(3, 3) X(5, 5) X(9, 9) X(17, 17) X(3, 1) X(1, 3)

@@ -1,0 +1,362 @@
+// HBM-staged passes for the levels whose planes do not fit the LDS-resident kernels (n > 136,
+// e.g. BASELINE config c5: 256x256 bands, J=6 -> 384^2 and 192^2 levels).
+//
+// A big n x n level is transformed as a row pass then a column pass through HBM; each pass stages
+// a block of whole lines in LDS and runs the same LDS FFT engine (fft_lds.h, natural order).  The
+// kymatio steps around each transform are fused into the passes:
+//   k_big_rows (forward):  kRowPad   reflect-pad gather of the input plane, S0 row partials,
+//                                    mean removal (conditioning only, as k_prep)
+//                          kRowReal2 U1 - mean, two real rows packed per complex line, split into
+//                                    the two rows' Hermitian half spectra (as k_o1 step 4-5)
+//   k_big_rows (inverse):  kRowFold1 fold_{2^j1}(Xhat * psi0) (order-1 subsample_fourier)
+//                          kRowFold2 Hermitian fold_{2^(j2-j1)}(U1hat * psi2 pair), 2 paths
+//   k_big_cols:            kColStore plain column transform
+//                          kColModLp |.| * scale, optional U store, phi low-pass column partials
+//                                    V[q][a] = sum_p GMnat[p][a] |z[p][q]| and column sums
+//   k_big_final:           S[a][c] from the partials (+ U1 mean), emitted like the LDS kernels
+// SURVEY.md Appendix A.4; reference call sites train_and_save_model.py:359-376.
+#pragma once
+
+#include "wst_device.h"
+
+namespace wstbig {
+
+using wstdev::DevParams;
+
+constexpr int kBigMinN = wstfft::kMaxFamilyN;   // levels with n > kBigMinN are staged
+constexpr int kBigThreads = 256;
+constexpr int kColTile = 16;                    // columns per column-pass workgroup (128 B rows)
+
+enum RowMode { kRowPad = 0, kRowReal2 = 1, kRowFold1 = 2, kRowFold2 = 3 };
+enum ColMode { kColStore = 0, kColModLp = 1 };
+enum FinalMode { kFinalRows = 0, kFinalCols = 1 };
+
+// Arguments of one staged launch (POD, by value).
+struct BigArgs {
+    int mode;
+    int n;                       // transform size of this level
+    int lvl;                     // level r (twiddles, tap matrices)
+    int rows;                    // rows per workgroup (row pass)
+    int ncols;                   // columns of the array (n, or n/2 + 1 for half spectra)
+    int L;
+    long long img0;              // first plane of the chunk (output row)
+    // kRowPad
+    const float* in;
+    const float* mean;           // kRowPad: plane means; kRowReal2: (plane, l1) U1 means
+    float* tpart;                // kRowPad: S0 row partials (n x oms per plane)
+    // kRowFold1
+    const float2* xhat;
+    int j1;                      // kRowFold1: psi level-0 filters of scale j1; s = 2^j1
+    // kRowReal2
+    const float* ureal;          // U1 (n x n per array)
+    // kRowFold2
+    const float2* hsrc;          // half spectra at level j1 (n1 x (n1/2+1) per (plane, l1))
+    int n1, l1, j2;
+    int l1_fixed;                // >= 0: launch covers one l1 (arrays = plane * npair + pair)
+    const float2* psi2;          // pair 0 of (j2, j1) in the psi2 pool
+    long long pstride;           // n1^2 (pool stride between pairs)
+    const int* box;              // alias boxes of the pairs (s >= 4), stride n + n
+    int npair, npath;            // pairs / paths per (plane, l1)
+    // outputs
+    float2* dst;
+    float* uout;                 // kColModLp: U real (optional)
+    float* vpart;                // kColModLp: V[q][a] (n x oms per array)
+    float* csum;                 // kColModLp: column sums (n per array)
+    float scale;                 // kColModLp
+    const float* gnat;           // natural-order tap matrix: GN_0 (kRowPad) / GM_lvl (kColModLp)
+    int oms;                     // row stride of the tap matrices and of tpart / vpart
+};
+
+__device__ __forceinline__ const float2* level_tw(const DevParams& p, int r) {
+    return p.tw + p.tw_off[2 * r];
+}
+
+// --------------------------------------------------------------------------------------------
+// row pass
+// --------------------------------------------------------------------------------------------
+// LDS: twiddles (N) | lines (nlines x ld, ld = N | 1) | scratch.
+template <int N, bool INV>
+__global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int ld = N | 1;
+    float2* tw = reinterpret_cast<float2*>(smem);
+    float2* A = tw + N;
+    const int T = blockDim.x;
+    const int arr = blockIdx.y;
+    const int r0 = blockIdx.x * a.rows;
+    const float2* gtw = level_tw(p, a.lvl);
+    for (int i = threadIdx.x; i < N; i += T) tw[i] = gtw[i];
+    int nlines = a.rows;
+
+    if (a.mode == kRowPad) {
+        // arr = chunk-local plane; raw values first (S0 partials), then mean-centred
+        const int inM = p.pre_pad ? p.PM : p.M, inN = p.pre_pad ? p.PN : p.N;
+        const float* x = a.in + static_cast<long long>(arr) * inM * inN;
+        for (int i = threadIdx.x; i < a.rows * N; i += T) {
+            const int rr = i / N, q = i - (i / N) * N;
+            const int u = r0 + rr;
+            const int su = p.pre_pad ? u : wstdev::reflect_index(u - p.padTop, p.M);
+            const int sv = p.pre_pad ? q : wstdev::reflect_index(q - p.padLeft, p.N);
+            A[rr * ld + q] = make_float2(x[su * inN + sv], 0.f);
+        }
+        __syncthreads();
+        // S0 row partials T[p][c] = sum_q GN0[q][c] x[p][q] (natural order), 8 lanes per output
+        for (int w = threadIdx.x; w < a.rows * p.oN * 8; w += T) {
+            const int qc = w & 7;
+            const int o = w >> 3;
+            const int rr = o / p.oN, c = o - (o / p.oN) * p.oN;
+            float acc = 0.f;
+            for (int q = qc; q < N; q += 8) acc = fmaf(a.gnat[q * a.oms + c], A[rr * ld + q].x, acc);
+#pragma unroll
+            for (int off = 4; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+            if (qc == 0) a.tpart[(static_cast<long long>(arr) * N + r0 + rr) * a.oms + c] = acc;
+        }
+        const float m = a.mean[arr];
+        __syncthreads();
+        for (int i = threadIdx.x; i < a.rows * N; i += T) {
+            const int rr = i / N, q = i - (i / N) * N;
+            A[rr * ld + q].x -= m;
+        }
+    } else if (a.mode == kRowReal2) {
+        // arr = (plane, l1); rows r0 .. r0 + rows - 1 packed in pairs
+        nlines = a.rows / 2;
+        const float* U = a.ureal + static_cast<long long>(arr) * N * N;
+        const float m = a.mean[arr];
+        for (int i = threadIdx.x; i < nlines * N; i += T) {
+            const int t = i / N, q = i - (i / N) * N;
+            const int u = r0 + 2 * t;
+            A[t * ld + q] = make_float2(U[u * N + q] - m, U[(u + 1) * N + q] - m);
+        }
+    } else if (a.mode == kRowFold1) {
+        // arr = plane * L + l1: rows of fold_s(Xhat * psi0_{j1, l1}), Xhat is (N s) x (N s)
+        const int plane = arr / a.L, l1 = arr - (arr / a.L) * a.L;
+        const int s = 1 << a.j1;
+        const int PN = N * s;
+        const float2* X = a.xhat + static_cast<long long>(plane) * PN * PN;
+        const float* psi0 = p.psi + p.psi_off[(a.j1 * a.L + l1) * p.J + 0];
+        for (int i = threadIdx.x; i < a.rows * N; i += T) {
+            const int rr = i / N, q = i - (i / N) * N;
+            const int u = r0 + rr;
+            float2 acc = make_float2(0.f, 0.f);
+            for (int ii = 0; ii < s; ++ii)
+                for (int jj = 0; jj < s; ++jj) {
+                    const long long idx = static_cast<long long>(u + ii * N) * PN + q + jj * N;
+                    const float f = psi0[idx];
+                    const float2 xv = X[idx];
+                    acc = make_float2(fmaf(xv.x, f, acc.x), fmaf(xv.y, f, acc.y));
+                }
+            A[rr * ld + q] = acc;
+        }
+    } else {  // kRowFold2
+        // arr = plane * npair + pair (one l1 per launch); two paths per pair -> 2 * rows lines
+        nlines = 2 * a.rows;
+        const int plane = arr / a.npair, pr = arr - (arr / a.npair) * a.npair;
+        const int n1 = a.n1, hld = n1 / 2 + 1, half = n1 / 2;
+        const int s = n1 / N, smask = s - 1;
+        const float2* H = a.hsrc + (static_cast<long long>(plane) * a.L + a.l1) * n1 * hld;
+        const float2* ps = a.psi2 + pr * a.pstride;
+        const int* bx = a.box + pr * (N + N);
+        for (int i = threadIdx.x; i < a.rows * N; i += T) {
+            const int rr = i / N, v = i - (i / N) * N;
+            const int u = r0 + rr;
+            int i0 = 0, ni = s, j0 = 0, nj = s;
+            if (bx && s >= 4) {
+                const int rb = bx[u], cb = bx[N + v];
+                i0 = rb & 255; ni = rb >> 8; j0 = cb & 255; nj = cb >> 8;
+            }
+            float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+            for (int ii = 0; ii < ni; ++ii) {
+                const int kr = u + ((i0 + ii) & smask) * N;
+                const int krm = kr == 0 ? 0 : n1 - kr;
+                for (int jj = 0; jj < nj; ++jj) {
+                    const int kc = v + ((j0 + jj) & smask) * N;
+                    const bool mir = kc > half;
+                    float2 h = H[mir ? krm * hld + (n1 - kc) : kr * hld + kc];
+                    h.y = mir ? -h.y : h.y;
+                    const float2 f = ps[static_cast<long long>(kr) * n1 + kc];
+                    a0 = make_float2(fmaf(h.x, f.x, a0.x), fmaf(h.y, f.x, a0.y));
+                    a1 = make_float2(fmaf(h.x, f.y, a1.x), fmaf(h.y, f.y, a1.y));
+                }
+            }
+            A[rr * ld + v] = a0;
+            A[(a.rows + rr) * ld + v] = a1;
+        }
+    }
+    __syncthreads();
+    wstfft::EpiIdentity id;
+    wstfft::fft_lines<N, INV>(A, wstfft::Lines(1, 0, nlines, ld, 1), tw, id);
+
+    if (a.mode == kRowPad || a.mode == kRowFold1) {
+        float2* D = a.dst + static_cast<long long>(arr) * N * N;
+        for (int i = threadIdx.x; i < a.rows * N; i += T) {
+            const int rr = i / N, q = i - (i / N) * N;
+            D[(r0 + rr) * N + q] = A[rr * ld + q];
+        }
+    } else if (a.mode == kRowReal2) {
+        constexpr int hld = N / 2 + 1;
+        float2* D = a.dst + static_cast<long long>(arr) * N * hld;
+        for (int i = threadIdx.x; i < nlines * hld; i += T) {
+            const int t = i / hld, q = i - (i / hld) * hld;
+            const float2 z = A[t * ld + q];
+            const float2 zm = A[t * ld + (q == 0 ? 0 : N - q)];
+            const int u = r0 + 2 * t;
+            D[u * hld + q] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+            D[(u + 1) * hld + q] = make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
+        }
+    } else {
+        // paths 2 pr, 2 pr + 1 of (plane, l1): dst arrays plane * npath + path
+        const int plane = arr / a.npair, pr = arr - (arr / a.npair) * a.npair;
+        for (int b = 0; b < 2; ++b) {
+            const int path = 2 * pr + b;
+            if (path >= a.npath) break;
+            float2* D = a.dst + (static_cast<long long>(plane) * a.npath + path) * N * N;
+            for (int i = threadIdx.x; i < a.rows * N; i += T) {
+                const int rr = i / N, q = i - (i / N) * N;
+                D[(r0 + rr) * N + q] = A[(b * a.rows + rr) * ld + q];
+            }
+        }
+    }
+}
+
+// --------------------------------------------------------------------------------------------
+// column pass: kColTile columns of one array per workgroup, each column contiguous in LDS
+// --------------------------------------------------------------------------------------------
+template <int N, bool INV>
+__global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int ld = N | 1;
+    constexpr int C = kColTile;
+    float2* tw = reinterpret_cast<float2*>(smem);
+    float2* A = tw + N;
+    const int T = blockDim.x;
+    const int arr = blockIdx.y;
+    const int c0 = blockIdx.x * C;
+    const int nc = min(C, a.ncols - c0);
+    const float2* gtw = level_tw(p, a.lvl);
+    for (int i = threadIdx.x; i < N; i += T) tw[i] = gtw[i];
+    float2* src = a.dst + static_cast<long long>(arr) * N * a.ncols;
+    for (int i = threadIdx.x; i < N * C; i += T) {
+        const int u = i / C, c = i - (i / C) * C;
+        if (c < nc) A[c * ld + u] = src[static_cast<long long>(u) * a.ncols + c0 + c];
+    }
+    __syncthreads();
+    if (a.mode == kColStore) {
+        wstfft::EpiIdentity id;
+        wstfft::fft_lines<N, INV>(A, wstfft::Lines(1, 0, nc, ld, 1), tw, id);
+        for (int i = threadIdx.x; i < N * C; i += T) {
+            const int u = i / C, c = i - (i / C) * C;
+            if (c < nc) src[static_cast<long long>(u) * a.ncols + c0 + c] = A[c * ld + u];
+        }
+        return;
+    }
+    // kColModLp: |.| * scale in place (.x), then partials over the rows of each column
+    wstdev::EpiModulus mod{a.scale, 0.f};
+    wstfft::fft_lines<N, INV>(A, wstfft::Lines(1, 0, nc, ld, 1), tw, mod);
+    if (a.uout) {
+        float* U = a.uout + static_cast<long long>(arr) * N * N;
+        for (int i = threadIdx.x; i < N * C; i += T) {
+            const int u = i / C, c = i - (i / C) * C;
+            if (c < nc) U[static_cast<long long>(u) * N + c0 + c] = A[c * ld + u].x;
+        }
+    }
+    // V[q][a] = sum_p GMnat[p][a] m[p][q] (a < oM) and the column sum (a == oM slot): 8 lanes
+    // per (column, a), shuffle-reduced
+    const int oms = a.oms;
+    const float* GMn = a.gnat;
+    const int nouts = p.oM + 1;
+    for (int w = threadIdx.x; w < nc * nouts * 8; w += T) {
+        const int pc = w & 7;
+        const int o = w >> 3;
+        const int c = o / nouts, oa = o - (o / nouts) * nouts;
+        const float2* col = A + c * ld;
+        float acc = 0.f;
+        if (oa < p.oM) {
+            for (int u = pc; u < N; u += 8) acc = fmaf(GMn[u * oms + oa], col[u].x, acc);
+        } else {
+            for (int u = pc; u < N; u += 8) acc += col[u].x;
+        }
+#pragma unroll
+        for (int off = 4; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (pc == 0) {
+            if (oa < p.oM) a.vpart[(static_cast<long long>(arr) * N + c0 + c) * oms + oa] = acc;
+            else a.csum[static_cast<long long>(arr) * N + c0 + c] = acc;
+        }
+    }
+}
+
+// Size-independent kernels: defined in one object only (wst_staged.hip with WST_BIG_N = 0).
+#ifdef WST_BIG_COMMON_KERNELS
+// --------------------------------------------------------------------------------------------
+// plane means of the reflect-padded input (the conditioning of k_prep's FFT input)
+// --------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBigThreads) k_big_mean(DevParams p, const float* __restrict__ in,
+                                                          float* __restrict__ mean) {
+    __shared__ float red[16];
+    const int PM = p.PM, PN = p.PN;
+    const int inM = p.pre_pad ? PM : p.M, inN = p.pre_pad ? PN : p.N;
+    const float* x = in + static_cast<long long>(blockIdx.x) * inM * inN;
+    float part = 0.f;
+    for (int i = threadIdx.x; i < PM * PN; i += blockDim.x) {
+        const int u = i / PN, v = i - (i / PN) * PN;
+        const int su = p.pre_pad ? u : wstdev::reflect_index(u - p.padTop, p.M);
+        const int sv = p.pre_pad ? v : wstdev::reflect_index(v - p.padLeft, p.N);
+        part += x[su * inN + sv];
+    }
+    const float s = wstdev::block_sum(part, red);
+    if (threadIdx.x == 0) mean[blockIdx.x] = s / (static_cast<float>(PM) * static_cast<float>(PN));
+}
+
+// --------------------------------------------------------------------------------------------
+// final low-pass contraction + emit, one workgroup per array
+//   kFinalRows: S[a][c] = sum_p G[p][a] T[p][c]   (T = S0 row partials, G = GMnat level 0)
+//   kFinalCols: S[a][c] = sum_q G[q][c] V[q][a]   (V = column partials, G = GNnat level lvl)
+// Coefficient of array `arr`: kind 0 -> k = 0 (plane = arr); 1 -> S1 (arr = plane*L + l1,
+// k = 1 + j1 L + l1); 2 -> S2 (arr = plane*npath + l2 for one l1, k = o2_base + (j2-j1-1) L + l2).
+// With `mean_out`, the U1 mean (sum of the column sums / n^2) of the array is stored too.
+// --------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_big_final(DevParams p, int fmode, int kind, int n, int oms,
+                                                  const float* __restrict__ part,
+                                                  const float* __restrict__ G,
+                                                  const float* __restrict__ csum,
+                                                  float* __restrict__ mean_out, int L, int j1,
+                                                  int l1, int j2, int npath, long long img0,
+                                                  float* __restrict__ out, int pooled) {
+    __shared__ float S[64];
+    __shared__ float red[16];
+    const int arr = blockIdx.x;
+    const float* P = part + static_cast<long long>(arr) * n * oms;
+    const int nout = p.oM * p.oN;
+    for (int o = threadIdx.x; o < nout; o += blockDim.x) {
+        const int ra = o / p.oN, c = o - (o / p.oN) * p.oN;
+        float acc = 0.f;
+        if (fmode == kFinalRows)
+            for (int k = 0; k < n; ++k) acc = fmaf(G[k * oms + ra], P[k * oms + c], acc);
+        else
+            for (int k = 0; k < n; ++k) acc = fmaf(G[k * oms + c], P[k * oms + ra], acc);
+        S[o] = acc;
+    }
+    if (mean_out) {
+        float s = 0.f;
+        for (int q = threadIdx.x; q < n; q += blockDim.x) s += csum[static_cast<long long>(arr) * n + q];
+        s = wstdev::block_sum(s, red);
+        if (threadIdx.x == 0) mean_out[arr] = s / (static_cast<float>(n) * static_cast<float>(n));
+    }
+    __syncthreads();
+    long long plane;
+    int k;
+    if (kind == 0) {
+        plane = arr;
+        k = 0;
+    } else if (kind == 1) {
+        plane = arr / L;
+        k = 1 + j1 * L + (arr - (arr / L) * L);
+    } else {
+        plane = arr / npath;
+        k = p.o2_base[j1 * L + l1] + (j2 - j1 - 1) * L + (arr - (arr / npath) * npath);
+    }
+    wstdev::emit(S, 1, k, img0 + plane, p.K, p.oM, p.oN, out, pooled);
+}
+
+#endif  // WST_BIG_COMMON_KERNELS
+
+}  // namespace wstbig

@@ -72,7 +72,7 @@ def scatter_device(x, M, N, J, L, max_order, pre_pad, pooled=False, out=None):
         raise RuntimeError(f"out must be a contiguous float32 tensor of shape {shape}")
     if B == 0:
         return out
-    planes = min(B, WORKSPACE_PLANES)
+    planes = min(B, WORKSPACE_PLANES, plan.preferred_batch())
     ws_bytes = plan.workspace_bytes(planes)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
     stream = torch.cuda.current_stream(x.device).cuda_stream
