@@ -128,6 +128,53 @@ int wst_host_filter(int M, int N, int J, int L, int kind, int j, int l, int r, d
 int wst_host_fft_lines(int n, int inverse, int mode, float* data, int nb, int bs, int nl, int ls,
                        int es, int threads, int* perm);
 
+/* ------------------------------------------------------------------------------------------
+ * Operators either side of the path (csrc/wst_aux.hip).
+ * ------------------------------------------------------------------------------------------ */
+
+/* Noise types of src/preprocessing/add_noise.py:14-72 (process_image's noise_type strings). */
+enum wst_noise_type {
+    WST_NOISE_GAUSSIAN = 0,        /* add_gaussian_noise        (:14-21)  */
+    WST_NOISE_SALT_AND_PEPPER = 1, /* add_salt_and_pepper_noise (:23-42)  */
+    WST_NOISE_SPECKLE = 2,         /* add_speckle_noise         (:44-53)  */
+    WST_NOISE_POISSON = 3,         /* add_poisson_noise         (:55-63)  */
+    WST_NOISE_UNIFORM = 4          /* add_uniform_noise         (:65-71)  */
+};
+
+/* Salt / pepper coordinate counts of add_noise.py:30,36: ceil(I/100 * H*W*C * 0.5) each. */
+int wst_salt_pepper_counts(int H, int W, int C, double intensity, int64_t* n_salt, int64_t* n_pepper);
+
+/*
+ * The add_noise.py formulas on caller-supplied draws (float64, same operation order, clip to
+ * [0, 255] then truncation to uint8) -- bit-exact with the reference given the same draws.
+ *   d_in    : device uint8, nimg x H x W x C (PIL HWC arrays).
+ *   d_draws : device float64, same shape: the N(0, I*255/100) gauss (gaussian), randn (speckle),
+ *             poisson draws (poisson), U(-r/2, r/2) noise (uniform); unused for salt & pepper.
+ *   d_salt_rc / d_pepper_rc : device int32, nimg x 2 x count (rows, then columns), counts from
+ *             wst_salt_pepper_counts; salt is applied first, then pepper, to every channel.
+ *   out_kind: 0 -> uint8 HWC (what add_noise.py saves); 1 -> float32 CHW / 255 (load_rgb_image,
+ *             train_and_save_model.py:51-56: the WST input).
+ */
+int wst_noise_apply(int noise_type, double intensity, const uint8_t* d_in, int64_t nimg, int H, int W,
+                    int C, const double* d_draws, const int32_t* d_salt_rc, const int32_t* d_pepper_rc,
+                    int out_kind, void* d_out, void* stream);
+
+/* Same formulas on on-device Philox4x32-10 draws keyed by (seed, image, element): the
+ * production path of the c4 noise sweep (numpy's MT19937 stream is not reproduced). */
+int wst_noise_generate(int noise_type, double intensity, const uint8_t* d_in, int64_t nimg, int H,
+                       int W, int C, uint64_t seed, int out_kind, void* d_out, void* stream);
+
+/*
+ * advanced_stats of src/training/train_and_save_model.py:58-112 per float32 plane (H*W <= 16384):
+ * d_out[plane][0..17] = mean, std, var, min, max, range, skew, kurt, cv, p10, p25, p50, p75, p90,
+ * iqr, mad, grad_mean, edge_density (float64).  Percentiles, sobel / laplace and the edge density
+ * reproduce numpy / scipy's float32 arithmetic exactly; moments are computed in float64.
+ */
+int wst_advanced_stats(const float* d_in, int64_t nplanes, int H, int W, double* d_out, void* stream);
+
+/* Thread-local message of the last failed wst_noise_* / wst_advanced_stats call. */
+const char* wst_aux_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,6 +24,8 @@ EXPORTS = (
     "wst_output_shape", "wst_padded_shape", "wst_workspace_bytes", "wst_preferred_batch",
     "wst_forward",
     "wst_forward_profiled", "wst_host_filter", "wst_host_fft_lines",
+    "wst_salt_pepper_counts", "wst_noise_apply", "wst_noise_generate", "wst_advanced_stats",
+    "wst_aux_last_error",
 )
 
 _lib = None
@@ -67,6 +69,20 @@ def load() -> ctypes.CDLL:
         lib.wst_padded_shape.argtypes = [c_vp] + [ctypes.POINTER(c_int)] * 2
         lib.wst_workspace_bytes.restype = c_int
         lib.wst_workspace_bytes.argtypes = [c_vp, c_i64, ctypes.POINTER(c_sz)]
+        u8p, f64p, i32p = ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p
+        lib.wst_salt_pepper_counts.restype = c_int
+        lib.wst_salt_pepper_counts.argtypes = [c_int, c_int, c_int, ctypes.c_double,
+                                               ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]
+        lib.wst_noise_apply.restype = c_int
+        lib.wst_noise_apply.argtypes = [c_int, ctypes.c_double, u8p, c_i64, c_int, c_int, c_int,
+                                        f64p, i32p, i32p, c_int, c_vp, c_vp]
+        lib.wst_noise_generate.restype = c_int
+        lib.wst_noise_generate.argtypes = [c_int, ctypes.c_double, u8p, c_i64, c_int, c_int, c_int,
+                                           ctypes.c_uint64, c_int, c_vp, c_vp]
+        lib.wst_advanced_stats.restype = c_int
+        lib.wst_advanced_stats.argtypes = [c_vp, c_i64, c_int, c_int, c_vp, c_vp]
+        lib.wst_aux_last_error.restype = ctypes.c_char_p
+        lib.wst_aux_last_error.argtypes = []
         lib.wst_preferred_batch.restype = c_int
         lib.wst_preferred_batch.argtypes = [c_vp, ctypes.POINTER(c_i64)]
         lib.wst_forward.restype = c_int
@@ -88,6 +104,16 @@ def load() -> ctypes.CDLL:
 
 def last_error() -> str:
     return load().wst_last_error().decode(errors="replace")
+
+
+def aux_last_error() -> str:
+    return (load().wst_aux_last_error() or b"").decode()
+
+
+def check_aux(code: int) -> None:
+    """Status check of the wst_noise_* / wst_advanced_stats entry points."""
+    if code != WST_OK:
+        raise WSTError(code, aux_last_error() or f"wst status {code}")
 
 
 def check(code: int) -> None:
