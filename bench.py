@@ -41,10 +41,24 @@ CONFIGS = {
                C=3, M=64, N=64, J=4, L=8, batch=1024),
     "c1": dict(workload="c1: 64x64 RGB patch, J=2 L=8 order-2 (batch as given)",
                C=3, M=64, N=64, J=2, L=8, batch=1024),
+    "c3": dict(workload="c3: 1M synthetic 64x64 RGB patches (generated on device) sharded over the "
+                        "ranks, J=4 L=8 order-2 pooled features + RCCL all-gather (one job per step)",
+               C=3, M=64, N=64, J=4, L=8, batch=1024, total=1_000_000),
+    "c4": dict(workload="c4: noise-robustness sweep -- 13 (type, intensity) cases of the reference's "
+                        "experiments/ (add_noise.py formulas, device draws) on 1024 64x64 RGB patches, "
+                        "each -> J=4 L=8 order-2 pooled features (per GPU)",
+               C=3, M=64, N=64, J=4, L=8, batch=1024),
     "c5": dict(workload="c5: 64 x 256x256 4-band patches, Scattering2D J=6 L=12 order-2 (per GPU; "
                         "384^2 and 192^2 levels HBM-staged)",
                C=4, M=256, N=256, J=6, L=12, batch=64),
 }
+
+
+# the reference's noise sweep: experiments/<type>/*/datasets_<type>_<I>
+NOISE_SWEEP = [("gaussian", 30), ("gaussian", 50), ("poisson", 40), ("poisson", 60),
+               ("salt_and_pepper", 5), ("salt_and_pepper", 15), ("salt_and_pepper", 25),
+               ("speckle", 15), ("speckle", 35), ("speckle", 55),
+               ("uniform", 10), ("uniform", 25), ("uniform", 40)]
 
 
 def fft_flops(n1, n2):
@@ -222,6 +236,52 @@ def main():
     def step():
         plan.forward(x.data_ptr(), planes, out.data_ptr(), args.pooled, ws.data_ptr(), ws_bytes, stream)
 
+    units_per_step = B                    # patches one rank processes per step
+    extra = {}
+    if args.config == "c4":
+        from wst_amd import noise as wnoise
+        lib = _lib.load()
+        x_u8 = torch.from_numpy(rng.integers(0, 256, (B, M, N, C), dtype=np.uint8)).to(dev)
+        xin = torch.empty((B, C, M, N), dtype=torch.float32, device=dev)
+        feats = torch.empty((len(NOISE_SWEEP), planes, 2 * K), dtype=torch.float32, device=dev)
+        counter = [0]
+
+        def step():  # noqa: F811
+            counter[0] += 1
+            for i, (nt, inten) in enumerate(NOISE_SWEEP):
+                _lib.check_aux(lib.wst_noise_generate(wnoise.NOISE_TYPES[nt], float(inten), x_u8.data_ptr(),
+                                                      B, M, N, C, 1000 * counter[0] + i, 1, xin.data_ptr(),
+                                                      stream))
+                plan.forward(xin.data_ptr(), planes, feats[i].data_ptr(), True, ws.data_ptr(), ws_bytes,
+                             stream)
+        units_per_step = B * len(NOISE_SWEEP)
+        extra["sweep"] = [f"{t}_{i}" for t, i in NOISE_SWEEP]
+    elif args.config == "c3":
+        total = cfg["total"]
+        shard = (total + world - 1) // world
+        lo = min(total, rank * shard)
+        mine = min(total, lo + shard) - lo
+        feats = torch.empty((shard * C, 2 * K), dtype=torch.float32, device=dev)
+        allf = torch.empty((world * shard * C, 2 * K), dtype=torch.float32, device=dev) if world > 1 else None
+        gen = torch.Generator(device=dev)
+        xb_u8 = torch.empty((B, C, M, N), dtype=torch.uint8, device=dev)
+        xb = torch.empty((B, C, M, N), dtype=torch.float32, device=dev)
+
+        def step():  # noqa: F811
+            gen.manual_seed(1_000_003 * (rank + 1))
+            for b0 in range(0, mine, B):
+                nb = min(B, mine - b0)
+                torch.randint(0, 256, (nb, C, M, N), generator=gen, dtype=torch.uint8, device=dev,
+                              out=xb_u8[:nb])
+                torch.div(xb_u8[:nb], 255.0, out=xb[:nb])
+                plan.forward(xb.data_ptr(), nb * C, feats[b0 * C:].data_ptr(), True, ws.data_ptr(),
+                             ws_bytes, stream)
+            if world > 1:
+                dist.all_gather_into_tensor(allf, feats)
+        units_per_step = mine
+        extra["c3"] = {"total_patches": total, "patches_this_rank": mine,
+                       "gathered_bytes": (world * shard * C * 2 * K * 4) if world > 1 else 0}
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -240,7 +300,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
     ms_per_step = dt / args.steps * 1e3
-    value = B * world * args.steps / dt
+    if args.config == "c3":
+        value = cfg["total"] * args.steps / dt
+    else:
+        value = units_per_step * world * args.steps / dt
 
     # per-kernel HIP-event durations on the launch stream (separate, untimed passes)
     slots = kernel_slots(J)
@@ -304,14 +367,16 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic uint8/255 RGB patches (load_rgb_image distribution), resident in HBM",
-            "config": {"workload": cfg["workload"], "patches_per_gpu": B, "channels": C,
+            "config": {"workload": cfg["workload"], "patches_per_gpu": units_per_step, "channels": C,
                        "shape": [M, N], "J": J, "L": L, "max_order": 2, "K": K,
-                       "output": "pooled [mean|std]" if args.pooled else f"full ({K},{Mo},{No}) fp32",
+                       "output": ("pooled [mean|std]" if (args.pooled or args.config in ("c3", "c4"))
+                                  else f"full ({K},{Mo},{No}) fp32"),
                        "parallelism": f"patch-sharded x{world} (no collective in step)"},
             "roofline": roofline, "step_roofline": step_roof, "cpu_baseline": cpu,
         }
         if gather:
             line["gather"] = gather
+        line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
