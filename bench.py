@@ -257,12 +257,11 @@ def main():
         units_per_step = B * len(NOISE_SWEEP)
         extra["sweep"] = [f"{t}_{i}" for t, i in NOISE_SWEEP]
     elif args.config == "c3":
+        from wst_amd import distributed as wdist
         total = cfg["total"]
-        shard = (total + world - 1) // world
-        lo = min(total, rank * shard)
-        mine = min(total, lo + shard) - lo
-        feats = torch.empty((shard * C, 2 * K), dtype=torch.float32, device=dev)
-        allf = torch.empty((world * shard * C, 2 * K), dtype=torch.float32, device=dev) if world > 1 else None
+        lo, hi = wdist.shard_range(total, rank, world)
+        mine = hi - lo
+        feats = torch.empty((mine * C, 2 * K), dtype=torch.float32, device=dev)
         gen = torch.Generator(device=dev)
         xb_u8 = torch.empty((B, C, M, N), dtype=torch.uint8, device=dev)
         xb = torch.empty((B, C, M, N), dtype=torch.float32, device=dev)
@@ -276,11 +275,11 @@ def main():
                 torch.div(xb_u8[:nb], 255.0, out=xb[:nb])
                 plan.forward(xb.data_ptr(), nb * C, feats[b0 * C:].data_ptr(), True, ws.data_ptr(),
                              ws_bytes, stream)
-            if world > 1:
-                dist.all_gather_into_tensor(allf, feats)
+            if world > 1:   # RCCL all-gather of every rank's pooled features (padded shards)
+                wdist.gather_shards(feats.view(mine, C * 2 * K), total)
         units_per_step = mine
         extra["c3"] = {"total_patches": total, "patches_this_rank": mine,
-                       "gathered_bytes": (world * shard * C * 2 * K * 4) if world > 1 else 0}
+                       "gathered_bytes": total * C * 2 * K * 4 if world > 1 else 0}
 
     for _ in range(args.warmup):
         step()
