@@ -100,11 +100,11 @@ def rocprof_name(slot, PM, PN, J):
         return o if o in (1, 3, 5, 9, 17) and P <= 136 else 0
     fm, fn = fam(PM), fam(PN)
     if slot == "k_prep":
-        return f"k_prep<{fm}, {fn}>"
+        return f"k_prep<{fm}, {fn}"
     kind, j1 = slot.split("_j1=")
     n = max(PM, PN) >> int(j1)
     cap = 12 if n <= 12 else 24 if n <= 24 else 48 if n <= 48 else 136
-    return f"{kind}<{fm}, {fn}, {cap}>"
+    return f"{kind}<{fm}, {fn}, {cap}"
 
 
 def lib_sha():
@@ -143,8 +143,12 @@ def pmc_traffic(sha, kernel):
             except Exception:
                 continue
             per = d.get("hbm_bytes_per_launch", {})
-            if sha in (d.get("lib_sha"), d.get("src_sha")) and kernel in per:
-                return per[kernel]
+            if sha not in (d.get("lib_sha"), d.get("src_sha")):
+                continue
+            # `kernel` is the template prefix "k_o2<3, 3, 136"; variants append ", SQ, HG>"
+            for name, v in per.items():
+                if name == kernel + ">" or name.startswith(kernel + ","):
+                    return v
     return None
 
 
@@ -322,7 +326,7 @@ def main():
     dname = rocprof_name(dom, plan.PM, plan.PN, J)
     roofline = {
         "bound": "mfma", "pipe": "fp32 (VALU FFT butterflies; gfx950 f32 MFMA shares the 157.3 TFLOP/s peak)",
-        "kernel": f"{dom} ({dname})", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
+        "kernel": f"{dom} ({dname}, ...>)", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
         "traffic": pmc_traffic(sha, dname) or pmc_traffic(lib_sha(), dname),
         "launches_per_step": nchunks,
