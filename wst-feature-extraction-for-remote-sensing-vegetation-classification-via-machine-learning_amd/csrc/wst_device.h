@@ -642,33 +642,52 @@ __device__ __forceinline__ void fold2_s2(const float2* H, int hld, int nM1, int 
                                          int nM2, int nN2) {
     const int items = nM2 * nN2;
     const int total = npair * items;
+    const int T = blockDim.x;
     const wstfft::FastDiv ditems(items), dn(nN2);
-    for (int w = threadIdx.x; w < total; w += blockDim.x) {
-        const int pr = ditems.div(w);
-        const int it = w - pr * items;
-        const int u = dn.div(it), v = it - u * nN2;
-        const float2* ps = psi2 + pr * pstride;
-        const int r0 = u, r1 = u + nM2;
-        const int m0 = u == 0 ? 0 : nM1 - u, m1 = nM2 - u;
-        // column v + nN2: mirrored index (nN2 - v) in row krm, or direct column nN2 when v == 0
-        const int cm = nN2 - v;
-        const int a01 = v == 0 ? r0 * hld + nN2 : m0 * hld + cm;
-        const int a11 = v == 0 ? r1 * hld + nN2 : m1 * hld + cm;
-        const float sg = v == 0 ? 1.f : -1.f;
-        const float2 h00 = H[r0 * hld + v], h10 = H[r1 * hld + v];
-        float2 h01 = H[a01], h11 = H[a11];
-        h01.y *= sg;
-        h11.y *= sg;
-        const float2 f00 = ps[r0 * nN1 + v], f01 = ps[r0 * nN1 + v + nN2];
-        const float2 f10 = ps[r1 * nN1 + v], f11 = ps[r1 * nN1 + v + nN2];
-        float2 a0, a1;
-        a0.x = fmaf(h00.x, f00.x, fmaf(h01.x, f01.x, fmaf(h10.x, f10.x, h11.x * f11.x)));
-        a0.y = fmaf(h00.y, f00.x, fmaf(h01.y, f01.x, fmaf(h10.y, f10.x, h11.y * f11.x)));
-        a1.x = fmaf(h00.x, f00.y, fmaf(h01.x, f01.y, fmaf(h10.x, f10.y, h11.x * f11.y)));
-        a1.y = fmaf(h00.y, f00.y, fmaf(h01.y, f01.y, fmaf(h10.y, f10.y, h11.y * f11.y)));
-        float2* dst = B + 2 * pr * pslot + u * ld2 + v;
-        dst[0] = a0;
-        if (2 * pr + 1 < npath) dst[pslot] = a1;
+    // two items per iteration: their 8 filter loads (L2) and 8 spectrum reads are in flight together
+    for (int w0 = threadIdx.x; w0 < total; w0 += 2 * T) {
+        float2 h[2][4], f[2][4];
+        int pr[2], u[2], v[2];
+        bool ok[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int w = w0 + k * T;
+            ok[k] = w < total;
+            const int ww = ok[k] ? w : w0;
+            pr[k] = ditems.div(ww);
+            const int it = ww - pr[k] * items;
+            u[k] = dn.div(it);
+            v[k] = it - u[k] * nN2;
+            const float2* ps = psi2 + pr[k] * pstride;
+            const int r0 = u[k], r1 = u[k] + nM2;
+            const int m0 = r0 == 0 ? 0 : nM1 - r0, m1 = nM2 - r0;
+            const int cm = nN2 - v[k];
+            const bool v0 = v[k] == 0;
+            h[k][0] = H[r0 * hld + v[k]];
+            h[k][1] = H[v0 ? r0 * hld + nN2 : m0 * hld + cm];
+            h[k][2] = H[r1 * hld + v[k]];
+            h[k][3] = H[v0 ? r1 * hld + nN2 : m1 * hld + cm];
+            f[k][0] = ps[r0 * nN1 + v[k]];
+            f[k][1] = ps[r0 * nN1 + v[k] + nN2];
+            f[k][2] = ps[r1 * nN1 + v[k]];
+            f[k][3] = ps[r1 * nN1 + v[k] + nN2];
+            if (!v0) {
+                h[k][1].y = -h[k][1].y;
+                h[k][3].y = -h[k][3].y;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            if (!ok[k]) continue;
+            float2 a0, a1;
+            a0.x = fmaf(h[k][0].x, f[k][0].x, fmaf(h[k][1].x, f[k][1].x, fmaf(h[k][2].x, f[k][2].x, h[k][3].x * f[k][3].x)));
+            a0.y = fmaf(h[k][0].y, f[k][0].x, fmaf(h[k][1].y, f[k][1].x, fmaf(h[k][2].y, f[k][2].x, h[k][3].y * f[k][3].x)));
+            a1.x = fmaf(h[k][0].x, f[k][0].y, fmaf(h[k][1].x, f[k][1].y, fmaf(h[k][2].x, f[k][2].y, h[k][3].x * f[k][3].y)));
+            a1.y = fmaf(h[k][0].y, f[k][0].y, fmaf(h[k][1].y, f[k][1].y, fmaf(h[k][2].y, f[k][2].y, h[k][3].y * f[k][3].y)));
+            float2* dst = B + 2 * pr[k] * pslot + u[k] * ld2 + v[k];
+            dst[0] = a0;
+            if (2 * pr[k] + 1 < npath) dst[pslot] = a1;
+        }
     }
 }
 
@@ -814,11 +833,15 @@ __global__ void __launch_bounds__(1024) k_o1(DevParams p, LdsLayout lay, int j1,
 // ------------------------------------------------------------------------------------------
 // k_o2: one workgroup per (plane, theta1) at fixed j1 -- all order-2 paths from U1hat
 // ------------------------------------------------------------------------------------------
+// Minimum waves per SIMD requested for k_o2 per size class (the VGPR budget follows): the small
+// levels run many workgroups per CU and gain from 5-6 waves (cap 48: 1.09 -> 0.98 ms at c2); the
+// 96^2 level is held at 2 workgroups per CU by LDS and spills below ~112 VGPRs (measured).
+constexpr int o2_min_waves(int cap) { return cap == 48 ? 6 : cap == 24 ? 5 : 1; }
 // HG = 1: the level-j1 spectrum is a big (HBM-staged, wst_staged.h) level: `hexp` holds the
 // fully transformed half spectra in natural order, the fold reads them from HBM (no LDS copy,
 // no column FFT) and the paths start at j2first (the first LDS-resident level).
 template <int FM, int FN, int MAXN, int SQ, int HG = 0>
-__global__ void __launch_bounds__(1024) k_o2(DevParams p, LdsLayout lay, int j1, int nimg,
+__global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, LdsLayout lay, int j1, int nimg,
                                              long long img0, const float2* __restrict__ hexp,
                                              float* __restrict__ out, int pooled, int j2first) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
