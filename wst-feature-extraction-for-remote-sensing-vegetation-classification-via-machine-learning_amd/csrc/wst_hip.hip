@@ -141,7 +141,7 @@ struct wst_plan {
     std::vector<LdsLayout> hg_lay;                // k_o2 (global spectrum) after a staged j1
     std::vector<size_t> hg_lds;
     std::vector<int> hg_threads, hg_j2first;
-    size_t big_rows_lds = 0, big_cols_lds = 0;
+    std::vector<size_t> big_rows_lds, big_cols_lds;   // per staged level (2 R lines / 16 columns)
     std::vector<size_t> ws_hbig;                  // U1hat half spectra of staged j1 (per plane)
     size_t ws_tmp = 0, ws_ureal = 0, ws_part = 0, ws_csum = 0, ws_mean = 0;
     int64_t max_chunk = 2048;                     // planes per workspace chunk
@@ -584,9 +584,14 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
             if (!(plan->big[r] = big_ops(g.PM >> r)))
                 return fail(WST_ERR_UNSUPPORTED, "no HBM-staged FFT compiled for level size " +
                                                      std::to_string(g.PM >> r));
-        const int nmax = g.PM;
-        plan->big_rows_lds = (nmax + 2 * kBigRows * (nmax | 1)) * sizeof(float2);
-        plan->big_cols_lds = (nmax + wstbig::kColTile * (nmax | 1)) * sizeof(float2);
+        plan->big_rows_lds.assign(plan->rb, 0);
+        plan->big_cols_lds.assign(plan->rb, 0);
+        for (int r = 0; r < plan->rb; ++r) {
+            const size_t n = static_cast<size_t>(g.PM >> r);
+            plan->big_rows_lds[r] = (n + 2 * kBigRows * (n | 1)) * sizeof(float2);
+            plan->big_cols_lds[r] = (n + wstbig::kColTile * (n | 1)) * sizeof(float2) +
+                                    n * static_cast<size_t>(oms) * sizeof(float);   // + tap matrix
+        }
     } else {
         plan->prep_lds = layout(plan->prep_lay, static_cast<size_t>(g.PM) * odd_ld(g.PN) * sizeof(float2),
                                 0, t, Blocks{0, 0, true}, 0, 0, omn);
@@ -651,7 +656,7 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
         plan->ws_csum = wsp;
         wsp += align16(part_n * sizeof(float));
         plan->ws_mean = wsp;
-        wsp += align16((1 + static_cast<size_t>(L)) * sizeof(float));
+        wsp += align16((wstbig::kMeanParts + static_cast<size_t>(L)) * sizeof(float));
     }
     for (int j1 = plan->rb; j1 < J; ++j1) {
         const int nM1 = g.PM >> j1, nN1 = g.PN >> j1;
@@ -819,8 +824,9 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
     float* ureal = reinterpret_cast<float*>(base + plan->ws_ureal * chunk);
     float* part = reinterpret_cast<float*>(base + plan->ws_part * chunk);
     float* csum = reinterpret_cast<float*>(base + plan->ws_csum * chunk);
-    float* mean = reinterpret_cast<float*>(base + plan->ws_mean * chunk);   // [plane] then [plane*L + l1]
-    float* umean = mean + nimg;
+    // [plane][kMeanParts] partial sums, then [plane * L + l1] U1 means
+    float* mean = reinterpret_cast<float*>(base + plan->ws_mean * chunk);
+    float* umean = mean + static_cast<size_t>(nimg) * kMeanParts;
     const dim3 tb(kBigThreads);
     auto gnat = [&](int r, int d) { return plan->d_lpn + plan->lpn_off[2 * r + d]; };
     auto args = [&](int mode, int r) {
@@ -838,7 +844,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
     int rc;
     // ---- S0 and Xhat (level 0) ----
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
-    cm.mean(Launch{dim3(nimg), tb, 0, stream}, dp, in, mean);
+    cm.mean(Launch{dim3(nimg, kMeanParts), tb, 0, stream}, dp, in, mean);
     {
         BigArgs a = args(kRowPad, 0);
         a.in = in;
@@ -846,10 +852,10 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         a.tpart = part;
         a.gnat = gnat(0, 1);
         a.dst = xhat;
-        plan->big[0]->rows(false, Launch{dim3(PM / kBigRows, nimg), tb, plan->big_rows_lds, stream}, dp, a);
+        plan->big[0]->rows(false, Launch{dim3(PM / kBigRows, nimg), tb, plan->big_rows_lds[0], stream}, dp, a);
         BigArgs c = args(kColStore, 0);
         c.dst = xhat;
-        plan->big[0]->cols(false, Launch{dim3((PM + kColTile - 1) / kColTile, nimg), tb, plan->big_cols_lds, stream},
+        plan->big[0]->cols(false, Launch{dim3((PM + kColTile - 1) / kColTile, nimg), tb, plan->big_cols_lds[0], stream},
                            dp, c);
         cm.final_(Launch{dim3(nimg), dim3(64), 0, stream}, dp, kFinalRows, 0, PM, plan->oms, part,
                   gnat(0, 0), nullptr, nullptr, L, 0, 0, 0, 1, img0, d_out, pooled);
@@ -868,7 +874,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         a.xhat = xhat;
         a.j1 = j1;
         a.dst = tmp;
-        B1->rows(true, Launch{dim3(n1 / kBigRows, nimg * L), tb, plan->big_rows_lds, stream}, dp, a);
+        B1->rows(true, Launch{dim3(n1 / kBigRows, nimg * L), tb, plan->big_rows_lds[j1], stream}, dp, a);
         BigArgs c = args(kColModLp, j1);
         c.dst = tmp;
         c.uout = do2 ? ureal : nullptr;
@@ -876,7 +882,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         c.csum = csum;
         c.scale = 1.f / (static_cast<float>(g.PM) * static_cast<float>(g.PN));
         c.gnat = gnat(j1, 0);
-        B1->cols(true, Launch{dim3((n1 + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds, stream},
+        B1->cols(true, Launch{dim3((n1 + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds[j1], stream},
                  dp, c);
         cm.final_(Launch{dim3(nimg * L), dim3(64), 0, stream}, dp, kFinalCols, 1, n1, plan->oms, part,
                   gnat(j1, 1), csum, do2 ? umean : nullptr, L, j1, 0, 0, 1, img0, d_out, pooled);
@@ -886,11 +892,11 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
             r2.ureal = ureal;
             r2.mean = umean;
             r2.dst = hbig;
-            B1->rows(false, Launch{dim3(n1 / kBigRows, nimg * L), tb, plan->big_rows_lds, stream}, dp, r2);
+            B1->rows(false, Launch{dim3(n1 / kBigRows, nimg * L), tb, plan->big_rows_lds[j1], stream}, dp, r2);
             BigArgs c2 = args(kColStore, j1);
             c2.ncols = hld;
             c2.dst = hbig;
-            B1->cols(false, Launch{dim3((hld + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds, stream},
+            B1->cols(false, Launch{dim3((hld + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds[j1], stream},
                      dp, c2);
         }
         WST_HIP_CHECK(hipGetLastError());
@@ -913,14 +919,14 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
                 f.npair = nq;
                 f.npath = L;
                 f.dst = tmp;
-                B2->rows(true, Launch{dim3(n2 / kBigRows, nimg * nq), tb, plan->big_rows_lds, stream}, dp, f);
+                B2->rows(true, Launch{dim3(n2 / kBigRows, nimg), tb, plan->big_rows_lds[j2], stream}, dp, f);
                 BigArgs m2 = args(kColModLp, j2);
                 m2.dst = tmp;
                 m2.vpart = part;
                 m2.csum = csum;
                 m2.scale = 1.f / (static_cast<float>(n1) * static_cast<float>(n1));
                 m2.gnat = gnat(j2, 0);
-                B2->cols(true, Launch{dim3((n2 + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds, stream},
+                B2->cols(true, Launch{dim3((n2 + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds[j2], stream},
                          dp, m2);
                 cm.final_(Launch{dim3(nimg * L), dim3(64), 0, stream}, dp, kFinalCols, 2, n2, plan->oms,
                           part, gnat(j2, 1), nullptr, nullptr, L, j1, l1, j2, L, img0, d_out, pooled);

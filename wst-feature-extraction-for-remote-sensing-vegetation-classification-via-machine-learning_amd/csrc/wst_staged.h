@@ -26,6 +26,7 @@ using wstdev::DevParams;
 constexpr int kBigMinN = wstfft::kMaxFamilyN;   // levels with n > kBigMinN are staged
 constexpr int kBigThreads = 256;
 constexpr int kColTile = 16;                    // columns per column-pass workgroup (128 B rows)
+constexpr int kMeanParts = 16;                  // k_big_mean partial sums per plane
 
 enum RowMode { kRowPad = 0, kRowReal2 = 1, kRowFold1 = 2, kRowFold2 = 3 };
 enum ColMode { kColStore = 0, kColModLp = 1 };
@@ -42,7 +43,8 @@ struct BigArgs {
     long long img0;              // first plane of the chunk (output row)
     // kRowPad
     const float* in;
-    const float* mean;           // kRowPad: plane means; kRowReal2: (plane, l1) U1 means
+    const float* mean;           // kRowPad: plane sum partials (kMeanParts per plane);
+                                 // kRowReal2: (plane, l1) U1 means
     float* tpart;                // kRowPad: S0 row partials (n x oms per plane)
     // kRowFold1
     const float2* xhat;
@@ -52,11 +54,11 @@ struct BigArgs {
     // kRowFold2
     const float2* hsrc;          // half spectra at level j1 (n1 x (n1/2+1) per (plane, l1))
     int n1, l1, j2;
-    int l1_fixed;                // >= 0: launch covers one l1 (arrays = plane * npair + pair)
     const float2* psi2;          // pair 0 of (j2, j1) in the psi2 pool
     long long pstride;           // n1^2 (pool stride between pairs)
     const int* box;              // alias boxes of the pairs (s >= 4), stride n + n
-    int npair, npath;            // pairs / paths per (plane, l1)
+    int npair, npath;            // pairs / paths per (plane, l1); one launch per l1, one
+                                 // workgroup per (plane, row block) loops over the pairs
     // outputs
     float2* dst;
     float* uout;                 // kColModLp: U real (optional)
@@ -111,7 +113,9 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
             for (int off = 4; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
             if (qc == 0) a.tpart[(static_cast<long long>(arr) * N + r0 + rr) * a.oms + c] = acc;
         }
-        const float m = a.mean[arr];
+        float msum = 0.f;   // plane mean from k_big_mean's partials, fixed order (deterministic)
+        for (int k = 0; k < kMeanParts; ++k) msum += a.mean[arr * kMeanParts + k];
+        const float m = msum / (static_cast<float>(p.PM) * static_cast<float>(p.PN));
         __syncthreads();
         for (int i = threadIdx.x; i < a.rows * N; i += T) {
             const int rr = i / N, q = i - (i / N) * N;
@@ -147,40 +151,53 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
                 }
             A[rr * ld + q] = acc;
         }
-    } else {  // kRowFold2
-        // arr = plane * npair + pair (one l1 per launch); two paths per pair -> 2 * rows lines
-        nlines = 2 * a.rows;
-        const int plane = arr / a.npair, pr = arr - (arr / a.npair) * a.npair;
+    } else {  // kRowFold2: arr = plane (one l1 per launch); every pair in turn, 2 paths each
         const int n1 = a.n1, hld = n1 / 2 + 1, half = n1 / 2;
         const int s = n1 / N, smask = s - 1;
-        const float2* H = a.hsrc + (static_cast<long long>(plane) * a.L + a.l1) * n1 * hld;
-        const float2* ps = a.psi2 + pr * a.pstride;
-        const int* bx = a.box + pr * (N + N);
-        for (int i = threadIdx.x; i < a.rows * N; i += T) {
-            const int rr = i / N, v = i - (i / N) * N;
-            const int u = r0 + rr;
-            int i0 = 0, ni = s, j0 = 0, nj = s;
-            if (bx && s >= 4) {
-                const int rb = bx[u], cb = bx[N + v];
-                i0 = rb & 255; ni = rb >> 8; j0 = cb & 255; nj = cb >> 8;
+        const float2* H = a.hsrc + (static_cast<long long>(arr) * a.L + a.l1) * n1 * hld;
+        wstfft::EpiIdentity id;
+        for (int pr = 0; pr < a.npair; ++pr) {
+            const float2* ps = a.psi2 + pr * a.pstride;
+            const int* bx = a.box + pr * (N + N);
+            for (int i = threadIdx.x; i < a.rows * N; i += T) {
+                const int rr = i / N, v = i - (i / N) * N;
+                const int u = r0 + rr;
+                int i0 = 0, ni = s, j0 = 0, nj = s;
+                if (bx && s >= 4) {
+                    const int rb = bx[u], cb = bx[N + v];
+                    i0 = rb & 255; ni = rb >> 8; j0 = cb & 255; nj = cb >> 8;
+                }
+                float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+                for (int ii = 0; ii < ni; ++ii) {
+                    const int kr = u + ((i0 + ii) & smask) * N;
+                    const int krm = kr == 0 ? 0 : n1 - kr;
+                    for (int jj = 0; jj < nj; ++jj) {
+                        const int kc = v + ((j0 + jj) & smask) * N;
+                        const bool mir = kc > half;
+                        float2 h = H[mir ? krm * hld + (n1 - kc) : kr * hld + kc];
+                        h.y = mir ? -h.y : h.y;
+                        const float2 f = ps[static_cast<long long>(kr) * n1 + kc];
+                        a0 = make_float2(fmaf(h.x, f.x, a0.x), fmaf(h.y, f.x, a0.y));
+                        a1 = make_float2(fmaf(h.x, f.y, a1.x), fmaf(h.y, f.y, a1.y));
+                    }
+                }
+                A[rr * ld + v] = a0;
+                A[(a.rows + rr) * ld + v] = a1;
             }
-            float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
-            for (int ii = 0; ii < ni; ++ii) {
-                const int kr = u + ((i0 + ii) & smask) * N;
-                const int krm = kr == 0 ? 0 : n1 - kr;
-                for (int jj = 0; jj < nj; ++jj) {
-                    const int kc = v + ((j0 + jj) & smask) * N;
-                    const bool mir = kc > half;
-                    float2 h = H[mir ? krm * hld + (n1 - kc) : kr * hld + kc];
-                    h.y = mir ? -h.y : h.y;
-                    const float2 f = ps[static_cast<long long>(kr) * n1 + kc];
-                    a0 = make_float2(fmaf(h.x, f.x, a0.x), fmaf(h.y, f.x, a0.y));
-                    a1 = make_float2(fmaf(h.x, f.y, a1.x), fmaf(h.y, f.y, a1.y));
+            __syncthreads();
+            wstfft::fft_lines<N, INV>(A, wstfft::Lines(1, 0, 2 * a.rows, ld, 1), tw, id);
+            for (int b = 0; b < 2; ++b) {
+                const int path = 2 * pr + b;
+                if (path >= a.npath) break;
+                float2* D = a.dst + (static_cast<long long>(arr) * a.npath + path) * N * N;
+                for (int i = threadIdx.x; i < a.rows * N; i += T) {
+                    const int rr = i / N, q = i - (i / N) * N;
+                    D[(r0 + rr) * N + q] = A[(b * a.rows + rr) * ld + q];
                 }
             }
-            A[rr * ld + v] = a0;
-            A[(a.rows + rr) * ld + v] = a1;
+            __syncthreads();
         }
+        return;
     }
     __syncthreads();
     wstfft::EpiIdentity id;
@@ -202,18 +219,6 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
             const int u = r0 + 2 * t;
             D[u * hld + q] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
             D[(u + 1) * hld + q] = make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
-        }
-    } else {
-        // paths 2 pr, 2 pr + 1 of (plane, l1): dst arrays plane * npath + path
-        const int plane = arr / a.npair, pr = arr - (arr / a.npair) * a.npair;
-        for (int b = 0; b < 2; ++b) {
-            const int path = 2 * pr + b;
-            if (path >= a.npath) break;
-            float2* D = a.dst + (static_cast<long long>(plane) * a.npath + path) * N * N;
-            for (int i = threadIdx.x; i < a.rows * N; i += T) {
-                const int rr = i / N, q = i - (i / N) * N;
-                D[(r0 + rr) * N + q] = A[(b * a.rows + rr) * ld + q];
-            }
         }
     }
 }
@@ -259,27 +264,36 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
             if (c < nc) U[static_cast<long long>(u) * N + c0 + c] = A[c * ld + u].x;
         }
     }
-    // V[q][a] = sum_p GMnat[p][a] m[p][q] (a < oM) and the column sum (a == oM slot): 8 lanes
-    // per (column, a), shuffle-reduced
+    // V[q][a] = sum_p GMnat[p][a] m[p][q] (a < oM <= 8) and the column sum: the taps are staged in
+    // LDS after the column tile, one thread per (column, 16-row chunk) accumulates
+    // every output of its rows, then the 16 chunks of a column are shuffle-reduced
     const int oms = a.oms;
-    const float* GMn = a.gnat;
-    const int nouts = p.oM + 1;
-    for (int w = threadIdx.x; w < nc * nouts * 8; w += T) {
-        const int pc = w & 7;
-        const int o = w >> 3;
-        const int c = o / nouts, oa = o - (o / nouts) * nouts;
+    float* G = reinterpret_cast<float*>(A + C * ld);   // N x oms taps after the column tile
+    for (int i = threadIdx.x; i < N * oms; i += T) G[i] = a.gnat[i];
+    __syncthreads();
+    constexpr int PC = 16;
+    for (int w = threadIdx.x; w < nc * PC; w += T) {
+        const int pc = w & (PC - 1);
+        const int c = w / PC;
         const float2* col = A + c * ld;
-        float acc = 0.f;
-        if (oa < p.oM) {
-            for (int u = pc; u < N; u += 8) acc = fmaf(GMn[u * oms + oa], col[u].x, acc);
-        } else {
-            for (int u = pc; u < N; u += 8) acc += col[u].x;
+        float acc[9];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc[k] = 0.f;
+        for (int u = pc; u < N; u += PC) {
+            const float m = col[u].x;
+            const float* g = G + u * oms;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (k < p.oM) acc[k] = fmaf(g[k], m, acc[k]);
+            acc[8] += m;
         }
 #pragma unroll
-        for (int off = 4; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        for (int off = PC / 2; off >= 1; off >>= 1)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) acc[k] += __shfl_xor(acc[k], off, 64);
         if (pc == 0) {
-            if (oa < p.oM) a.vpart[(static_cast<long long>(arr) * N + c0 + c) * oms + oa] = acc;
-            else a.csum[static_cast<long long>(arr) * N + c0 + c] = acc;
+            for (int k = 0; k < p.oM; ++k) a.vpart[(static_cast<long long>(arr) * N + c0 + c) * oms + k] = acc[k];
+            a.csum[static_cast<long long>(arr) * N + c0 + c] = acc[8];
         }
     }
 }
@@ -287,23 +301,26 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
 // Size-independent kernels: defined in one object only (wst_staged.hip with WST_BIG_N = 0).
 #ifdef WST_BIG_COMMON_KERNELS
 // --------------------------------------------------------------------------------------------
-// plane means of the reflect-padded input (the conditioning of k_prep's FFT input)
+// plane sums of the reflect-padded input, kMeanParts partials per plane (the conditioning mean of
+// k_prep's FFT input; kRowPad adds the partials in a fixed order)
 // --------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBigThreads) k_big_mean(DevParams p, const float* __restrict__ in,
-                                                          float* __restrict__ mean) {
+                                                          float* __restrict__ part) {
     __shared__ float red[16];
     const int PM = p.PM, PN = p.PN;
     const int inM = p.pre_pad ? PM : p.M, inN = p.pre_pad ? PN : p.N;
     const float* x = in + static_cast<long long>(blockIdx.x) * inM * inN;
-    float part = 0.f;
-    for (int i = threadIdx.x; i < PM * PN; i += blockDim.x) {
-        const int u = i / PN, v = i - (i / PN) * PN;
+    const int u0 = blockIdx.y * PM / kMeanParts, u1 = (blockIdx.y + 1) * PM / kMeanParts;
+    float s = 0.f;
+    for (int u = u0; u < u1; ++u) {
         const int su = p.pre_pad ? u : wstdev::reflect_index(u - p.padTop, p.M);
-        const int sv = p.pre_pad ? v : wstdev::reflect_index(v - p.padLeft, p.N);
-        part += x[su * inN + sv];
+        for (int v = threadIdx.x; v < PN; v += blockDim.x) {
+            const int sv = p.pre_pad ? v : wstdev::reflect_index(v - p.padLeft, p.N);
+            s += x[su * inN + sv];
+        }
     }
-    const float s = wstdev::block_sum(part, red);
-    if (threadIdx.x == 0) mean[blockIdx.x] = s / (static_cast<float>(PM) * static_cast<float>(PN));
+    s = wstdev::block_sum(s, red);
+    if (threadIdx.x == 0) part[blockIdx.x * kMeanParts + blockIdx.y] = s;
 }
 
 // --------------------------------------------------------------------------------------------
