@@ -28,6 +28,21 @@
 
 #include "fft_lds.h"
 
+// WST_STAMPS (diagnostic builds only): thread 0 of the first kStampBlocks workgroups of k_o2
+// records s_memtime at its phase boundaries into wst_stamps (read back by wst_dbg_stamps_*).
+#ifdef WST_STAMPS
+constexpr int kStampBlocks = 512, kStampSlots = 64;
+__device__ unsigned long long wst_stamps[kStampBlocks * kStampSlots];
+#define WST_STAMP(ctr)                                                                     \
+    do {                                                                                   \
+        if (stamp_on && threadIdx.x == 0 && blockIdx.x < kStampBlocks && (ctr) < kStampSlots)          \
+            wst_stamps[blockIdx.x * kStampSlots + (ctr)] = __builtin_amdgcn_s_memtime();   \
+        ++(ctr);                                                                           \
+    } while (0)
+#else
+#define WST_STAMP(ctr) do {} while (0)
+#endif
+
 namespace wstdev {
 
 constexpr int kMaxLds = 160 * 1024;
@@ -308,7 +323,8 @@ constexpr int kLpOM = 8;  // row stride of the GM tap matrices = largest oM of t
 template <int NN>
 __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, int ld,
                                            const float2* tw, const float* GM, const float* GN,
-                                           int oms, int oM, int oN, float scale, float* S) {
+                                           int oms, int oM, int oN, float scale, float* S,
+                                           float* outd) {
     using F = wstfft::LineFFT<NN, true>;
     constexpr bool single = (F::N2 == 1);
     constexpr int RU = single ? NN : F::N2;  // rows per unit
@@ -331,6 +347,27 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
         });
         wstfft::rfft<RU, true>(v);
         const float* gm = GM + (RU * k) * oms;
+        if constexpr (single) {
+            // whole column in one unit: the tap loads of a rolled loop over output-row pairs keep
+            // the register footprint to the RU moduli (unrolled, the RU x oms GM loads hoist)
+            float m[RU];
+            wstfft::static_for<0, RU>([&](auto ec) {
+                constexpr int e = decltype(ec)::value;
+                m[e] = __builtin_amdgcn_sqrtf(fmaf(v[e].x, v[e].x, v[e].y * v[e].y)) * scale;
+            });
+#pragma unroll 1
+            for (int t = 0; 2 * t < oM; ++t) {
+                float V0 = 0.f, V1 = 0.f;
+                wstfft::static_for<0, RU>([&](auto ec) {
+                    constexpr int e = decltype(ec)::value;
+                    const float2 g = *reinterpret_cast<const float2*>(gm + e * oms + 2 * t);
+                    V0 = fmaf(g.x, m[e], V0);
+                    V1 = fmaf(g.y, m[e], V1);
+                });
+                p[t * ld] = make_float2(V0, V1);
+            }
+            continue;
+        }
         float V[kLpOM];
 #pragma unroll
         for (int a = 0; a < kLpOM; ++a) V[a] = 0.f;
@@ -355,24 +392,10 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
             if (2 * t < oM) p[t * ld] = make_float2(V[2 * t], V[2 * t + 1]);
     }
     __syncthreads();
-    // 2. W over the units of each column (thread = (a, line), lanes along consecutive columns)
-    if constexpr (NU > 1) {
-        const wstfft::FastDiv dl(nlines);
-        for (int w = threadIdx.x; w < nlines * oM; w += T) {
-            const int a = dl.div(w);
-            const int line = w - a * nlines;
-            float* f = reinterpret_cast<float*>(U + g.offset(line) + (a >> 1) * ld) + (a & 1);
-            float acc = 0.f;
-            wstfft::static_for<0, NU>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                acc += f[2 * RU * k * ld];
-            });
-            *f = acc;
-        }
-        __syncthreads();
-    }
-    // 3. S = W GN
-    constexpr int QC = 8;
+    // 2+3. S = (sum_k V_k) GN in one pass: QC lanes split the columns q of output (b, a, c), each
+    //      sums the NU unit partials of its columns, shuffle reduction.  outd (nullable): write
+    //      S straight to the coefficient maps instead of S (non-pooled output).
+    constexpr int QC = NN >= 48 ? 16 : NN >= 24 ? 8 : NN >= 12 ? 4 : 2;   // ~3 columns per lane
     const int nout = nb * oM * oN;
     const wstfft::FastDiv dc(oN), dab(oM * oN);
     for (int w = threadIdx.x; w < nout * QC; w += T) {
@@ -384,10 +407,20 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
         const int c = ac - a * oN;
         const float* f = reinterpret_cast<const float*>(U + b * bs + (a >> 1) * ld) + (a & 1);
         float acc = 0.f;
-        for (int q = qc; q < cols; q += QC) acc = fmaf(GN[q * oms + c], f[2 * q], acc);
+        for (int q = qc; q < cols; q += QC) {
+            float wq = 0.f;
+            wstfft::static_for<0, NU>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                wq += f[2 * (q + RU * k * ld)];
+            });
+            acc = fmaf(GN[q * oms + c], wq, acc);
+        }
 #pragma unroll
         for (int off = QC / 2; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
-        if (qc == 0) S[o] = acc;
+        if (qc == 0) {
+            if (outd) outd[o] = acc;
+            else S[o] = acc;
+        }
     }
     __syncthreads();
 }
@@ -396,16 +429,16 @@ template <int FAM, int K, int HI>
 __device__ __forceinline__ void family_cols_modlp(float2* U, int nb, int bs, int rows, int cols,
                                                   int ld, const float2* tw, const float* GM,
                                                   const float* GN, int oms, int oM, int oN,
-                                                  float scale, float* S) {
+                                                  float scale, float* S, float* outd) {
     constexpr int NN = FAM << K;
     if constexpr (FAM > 0 && NN <= HI && NN <= wstfft::kMaxFamilyN) {
         if constexpr (NN >= 2) {
             if (rows == NN) {
-                cols_modlp<NN>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S);
+                cols_modlp<NN>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
                 return;
             }
         }
-        family_cols_modlp<FAM, K + 1, HI>(U, nb, bs, rows, cols, ld, tw, GM, GN, oms, oM, oN, scale, S);
+        family_cols_modlp<FAM, K + 1, HI>(U, nb, bs, rows, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
     }
 }
 
@@ -488,6 +521,21 @@ __device__ __forceinline__ Tables load_tables(const DevParams& p, const LdsLayou
 }
 
 __host__ __device__ inline int odd_ld(int n) { return n | 1; }
+
+// dst[i] = src[i] for i < n (global -> LDS): eight loads per thread in flight before the stores
+// (a plain loop waits out the HBM latency once per element).
+__device__ __forceinline__ void copy_to_lds(float2* dst, const float2* __restrict__ src, int n) {
+    constexpr int K = 8;
+    const int T = blockDim.x;
+    for (int i0 = threadIdx.x; i0 < n; i0 += K * T) {
+        float2 t[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) t[k] = src[min(i0 + k * T, n - 1)];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (i0 + k * T < n) dst[i0 + k * T] = t[k];
+    }
+}
 
 // Order-1 fold from HBM/L2: A[u][v] = sum_{i,j < s} X[u + i nM1][v + j nN1] * psi0[...]
 // S > 0: compile-time alias count; S == 0: runtime s.  U items per thread keep loads in flight.
@@ -590,6 +638,10 @@ __device__ __forceinline__ void fold2(const float2* H, int hld, int nM1, int nN1
     const int items = nM2 * nN2;
     const int total = npair * items;
     const wstfft::FastDiv ditems(items), dn(nN2);
+    // Taps are gathered in blocks of BR x BC aliases whose loads are all issued before the first
+    // is consumed (a tap outside the box re-reads the box's last row / column with weight 0), so
+    // a block costs one L2 round trip instead of one per tap.
+    constexpr int BR = 1, BC = 4;
     for (int w = threadIdx.x; w < total; w += blockDim.x) {
         const int pr = ditems.div(w);
         const int it = w - pr * items;
@@ -599,32 +651,37 @@ __device__ __forceinline__ void fold2(const float2* H, int hld, int nM1, int nN1
         const int rb = bx[u], cb = bx[nM2 + v];
         const int i0 = rb & 255, ni = rb >> 8, j0 = cb & 255, nj = cb >> 8;
         float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
-        auto row = [&](int i) {
-            const int kr = u + ((i0 + i) & smask) * nM2;
-            const int krm = kr == 0 ? 0 : nM1 - kr;
-            const float2* frow = ps + kr * nN1;
-            const float2* hrow = H + kr * hld;
-            const float2* hmir = H + krm * hld + nN1;
-            auto tap = [&](int j) {
-                const int kc = v + ((j0 + j) & smask) * nN2;
-                const bool mir = kc > half;
-                float2 a = mir ? hmir[-kc] : hrow[kc];
-                a.y = mir ? -a.y : a.y;
-                const float2 f = frow[kc];
-                a0 = make_float2(fmaf(a.x, f.x, a0.x), fmaf(a.y, f.x, a0.y));
-                a1 = make_float2(fmaf(a.x, f.y, a1.x), fmaf(a.y, f.y, a1.y));
-            };
-            // predicated blocks of up to 4 aliases keep the filter loads of a block in flight
-            for (int jb = 0; jb < nj; jb += 4) {
+        for (int ib = 0; ib < ni; ib += BR) {
+            for (int jb = 0; jb < nj; jb += BC) {
+                float2 hv[BR][BC], fv[BR][BC];
 #pragma unroll
-                for (int j2 = 0; j2 < (S == 2 ? 2 : 4); ++j2)
-                    if (jb + j2 < nj) tap(jb + j2);
+                for (int r = 0; r < BR; ++r) {
+                    const int kr = u + ((i0 + min(ib + r, ni - 1)) & smask) * nM2;
+                    const int krm = kr == 0 ? 0 : nM1 - kr;
+                    const float2* frow = ps + kr * nN1;
+                    const float2* hrow = H + kr * hld;
+                    const float2* hmir = H + krm * hld + nN1;
+#pragma unroll
+                    for (int c = 0; c < BC; ++c) {
+                        const int kc = v + ((j0 + min(jb + c, nj - 1)) & smask) * nN2;
+                        const bool mir = kc > half;
+                        float2 a = mir ? hmir[-kc] : hrow[kc];
+                        a.y = mir ? -a.y : a.y;
+                        hv[r][c] = a;
+                        fv[r][c] = frow[kc];
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < BR; ++r)
+#pragma unroll
+                    for (int c = 0; c < BC; ++c) {
+                        const bool ok = (ib + r < ni) && (jb + c < nj);
+                        const float2 f = ok ? fv[r][c] : make_float2(0.f, 0.f);
+                        const float2 a = hv[r][c];
+                        a0 = make_float2(fmaf(a.x, f.x, a0.x), fmaf(a.y, f.x, a0.y));
+                        a1 = make_float2(fmaf(a.x, f.y, a1.x), fmaf(a.y, f.y, a1.y));
+                    }
             }
-        };
-        for (int ib = 0; ib < ni; ib += 4) {
-#pragma unroll
-            for (int i2 = 0; i2 < (S == 2 ? 2 : 4); ++i2)
-                if (ib + i2 < ni) row(ib + i2);
         }
         float2* dst = B + 2 * pr * pslot + u * ld2 + v;
         dst[0] = a0;
@@ -758,11 +815,19 @@ __global__ void __launch_bounds__(1024) k_prep(DevParams p, LdsLayout lay,
 // kernel carries only those FFTs (code size stays well inside the instruction cache).
 constexpr int prev_cap(int c) { return c <= 12 ? 0 : c <= 24 ? 12 : c <= 48 ? 24 : 48; }
 
+// Minimum waves per SIMD for k_o1 per size class: the 96^2-class level runs 768-thread
+// workgroups, two per CU (LDS-bound), so it needs <= 80 VGPRs (6 waves per SIMD).
+// (families 3, 5, 9 square: the others' FFT sizes spill at that budget and keep 512 threads;
+// host side: o1_wide in wst_hip.hip)
+constexpr int o1_min_waves(int cap, int fm, int fn) {
+    return (cap == 136 && fm == fn && (fm == 3 || fm == 5 || fm == 9)) ? 6 : 1;
+}
+
 // ------------------------------------------------------------------------------------------
 // k_o1: one workgroup per (plane, theta1) at fixed j1 -- order 1 + half-spectrum export
 // ------------------------------------------------------------------------------------------
 template <int FM, int FN, int MAXN, int SQ>
-__global__ void __launch_bounds__(1024) k_o1(DevParams p, LdsLayout lay, int j1, int nimg,
+__global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevParams p, LdsLayout lay, int j1, int nimg,
                                              long long img0, const float2* __restrict__ xhat,
                                              float2* __restrict__ hexp, float* __restrict__ out,
                                              int pooled) {
@@ -860,6 +925,9 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
     const Tables tb = load_tables(p, lay, smem);
     const int dbg = p.dbg_skip;
     wstfft::EpiIdentity id;
+    [[maybe_unused]] int sctr = 0;
+    [[maybe_unused]] const bool stamp_on = (j1 == 0);
+    WST_STAMP(sctr);
     // order-2 path sizes: <= MAXN / 2 below an LDS-resident level of class MAXN, <= MAXN after a
     // big level
     constexpr int PHI = (SQ && !HG) ? MAXN / 2 : MAXN;
@@ -867,12 +935,13 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
     if constexpr (!HG) {
         // 1. half spectrum rows -> LDS, then the column FFTs (rows digit-reversed -> natural)
         float2* Hl = reinterpret_cast<float2*>(smem);
-        for (int o = threadIdx.x; o < nM1 * hld; o += blockDim.x) Hl[o] = Hg[o];
+        copy_to_lds(Hl, Hg, nM1 * hld);
         __syncthreads();
         if (!(dbg & 4))
             lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(
                 Hl, wstfft::Lines{1, 0, hld, 1, hld}, nM1, tb.twM(j1), id);
     }
+    WST_STAMP(sctr);
 
     // 2. order-2 paths in batches: Hermitian fold -> |ifft| -> S2 low-pass
     const int kbase = p.o2_base[j1 * L + l1];
@@ -893,17 +962,22 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
                 fold2_any(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
                           bx, nM2 + nN2);
             __syncthreads();
+            WST_STAMP(sctr);
             const float scale2 = 1.f / static_cast<float>(n1);
             if constexpr (SQ) {
                 // rows, then the column pass fused with |.| and the S2 low-pass
                 if (!(dbg & 16))
                     lds_fft_lines<FN, 0, PHI, kDR, true>(
                         B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, nN2, tb.twN(j2), id);
+                WST_STAMP(sctr);
+                const int k0 = kbase + (j2 - j1 - 1) * L + l2a;
+                float* outd = pooled ? nullptr : out + (img * p.K + k0) * (p.oM * p.oN);
                 if (!(dbg & 64))
                     family_cols_modlp<FM, 0, PHI>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
                                                        tb.gM(j2), tb.gN(j2), lay.oms, p.oM, p.oN,
-                                                       scale2, S);
-                emit(S, npath, kbase + (j2 - j1 - 1) * L + l2a, img, p.K, p.oM, p.oN, out, pooled);
+                                                       scale2, S, outd);
+                WST_STAMP(sctr);
+                if (!outd) emit(S, npath, k0, img, p.K, p.oM, p.oN, out, pooled);
             } else {
                 EpiModulus mod2{scale2, 0.f};
                 if (!(dbg & 16))
@@ -915,7 +989,8 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
                     emit(S, npath, kbase + (j2 - j1 - 1) * L + l2a, img, p.K, p.oM, p.oN, out, pooled);
                 }
             }
-            __syncthreads();
+            // no barrier here: the next batch's fold writes B only, and S is rewritten only after
+            // that batch's transform barriers (emit above reads S alone)
         }
     }
 }

@@ -664,6 +664,11 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
         const bool do2 = max_order >= 2 && j1 < J - 1;
         plan->cap[j1] = cap_for(std::max(nM1, nN1));
         plan->o1_threads[j1] = default_threads(n1);
+        // k_o1 of the 96^2 class in families 3/5/9 is built for 6 waves per SIMD
+        // (wst_device.h o1_min_waves): 768-thread workgroups, two per CU
+        if (plan->cap[j1] == 136 && plan->o1_threads[j1] == 512 && plan->fam_m == plan->fam_n &&
+            (plan->fam_m == 3 || plan->fam_m == 5 || plan->fam_m == 9))
+            plan->o1_threads[j1] = 768;
         plan->o2_threads[j1] = default_threads(n1);
         plan->o1_lds[j1] = layout(plan->o1_lay[j1], static_cast<size_t>(nM1) * odd_ld(nN1) * sizeof(float2),
                                   0, t, Blocks{j1, j1, !plan->sq}, j1, j1, omn);
