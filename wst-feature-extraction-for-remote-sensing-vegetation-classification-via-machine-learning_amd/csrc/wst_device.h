@@ -42,6 +42,9 @@ __device__ unsigned long long wst_stamps[kStampBlocks * kStampSlots];
 #else
 #define WST_STAMP(ctr) do {} while (0)
 #endif
+#ifndef WST_FOLD_IT
+#define WST_FOLD_IT 1  // box-sparse order-2 fold: items folded together per thread
+#endif
 
 namespace wstdev {
 
@@ -638,113 +641,145 @@ __device__ __forceinline__ void fold2(const float2* H, int hld, int nM1, int nN1
     const int items = nM2 * nN2;
     const int total = npair * items;
     const wstfft::FastDiv ditems(items), dn(nN2);
-    // Taps are gathered in blocks of BR x BC aliases whose loads are all issued before the first
-    // is consumed (a tap outside the box re-reads the box's last row / column with weight 0), so
-    // a block costs one L2 round trip instead of one per tap.
-    constexpr int BR = 1, BC = 4;
-    for (int w = threadIdx.x; w < total; w += blockDim.x) {
-        const int pr = ditems.div(w);
-        const int it = w - pr * items;
-        const int u = dn.div(it), v = it - u * nN2;
-        const float2* ps = psi2 + pr * pstride;
-        const int* bx = box + pr * bstride;
-        const int rb = bx[u], cb = bx[nM2 + v];
-        const int i0 = rb & 255, ni = rb >> 8, j0 = cb & 255, nj = cb >> 8;
-        float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
-        for (int ib = 0; ib < ni; ib += BR) {
-            for (int jb = 0; jb < nj; jb += BC) {
-                float2 hv[BR][BC], fv[BR][BC];
+    // IT items per thread are folded together and their taps gathered in blocks of BC column
+    // aliases per item, all loads of a block issued before the first is consumed (a tap outside
+    // an item's box re-reads its box's last row / column with weight 0), so one L2 round trip
+    // serves IT * BC taps.
+    constexpr int IT = WST_FOLD_IT, BC = 4;
+    const int T = blockDim.x;
+    for (int w0 = threadIdx.x; w0 < total; w0 += IT * T) {
+        int pr[IT], u[IT], v[IT], i0[IT], ni[IT], j0[IT], nj[IT];
+        int nimax = 0, njmax = 0;
 #pragma unroll
-                for (int r = 0; r < BR; ++r) {
-                    const int kr = u + ((i0 + min(ib + r, ni - 1)) & smask) * nM2;
+        for (int k = 0; k < IT; ++k) {
+            const int w = w0 + k * T;
+            const int ww = w < total ? w : w0;
+            pr[k] = ditems.div(ww);
+            const int it = ww - pr[k] * items;
+            u[k] = dn.div(it);
+            v[k] = it - u[k] * nN2;
+            const int* bx = box + pr[k] * bstride;
+            const int rb = bx[u[k]], cb = bx[nM2 + v[k]];
+            i0[k] = rb & 255;
+            j0[k] = cb & 255;
+            ni[k] = w < total ? rb >> 8 : 0;
+            nj[k] = cb >> 8;
+            nimax = max(nimax, ni[k]);
+            njmax = max(njmax, nj[k]);
+        }
+        float2 a0[IT], a1[IT];
+#pragma unroll
+        for (int k = 0; k < IT; ++k) a0[k] = a1[k] = make_float2(0.f, 0.f);
+        for (int ib = 0; ib < nimax; ++ib) {
+            for (int jb = 0; jb < njmax; jb += BC) {
+                float2 hv[IT][BC], fv[IT][BC];
+#pragma unroll
+                for (int k = 0; k < IT; ++k) {
+                    // (i0 + min(ib, ni - 1)) & smask stays a valid alias even for ni = 0
+                    const int kr = u[k] + ((i0[k] + min(ib, ni[k] - 1)) & smask) * nM2;
                     const int krm = kr == 0 ? 0 : nM1 - kr;
-                    const float2* frow = ps + kr * nN1;
+                    const float2* frow = psi2 + pr[k] * pstride + kr * nN1;
                     const float2* hrow = H + kr * hld;
                     const float2* hmir = H + krm * hld + nN1;
 #pragma unroll
                     for (int c = 0; c < BC; ++c) {
-                        const int kc = v + ((j0 + min(jb + c, nj - 1)) & smask) * nN2;
+                        const int kc = v[k] + ((j0[k] + min(jb + c, nj[k] - 1)) & smask) * nN2;
                         const bool mir = kc > half;
                         float2 a = mir ? hmir[-kc] : hrow[kc];
                         a.y = mir ? -a.y : a.y;
-                        hv[r][c] = a;
-                        fv[r][c] = frow[kc];
+                        hv[k][c] = a;
+                        fv[k][c] = frow[kc];
                     }
                 }
 #pragma unroll
-                for (int r = 0; r < BR; ++r)
+                for (int k = 0; k < IT; ++k)
 #pragma unroll
                     for (int c = 0; c < BC; ++c) {
-                        const bool ok = (ib + r < ni) && (jb + c < nj);
-                        const float2 f = ok ? fv[r][c] : make_float2(0.f, 0.f);
-                        const float2 a = hv[r][c];
-                        a0 = make_float2(fmaf(a.x, f.x, a0.x), fmaf(a.y, f.x, a0.y));
-                        a1 = make_float2(fmaf(a.x, f.y, a1.x), fmaf(a.y, f.y, a1.y));
+                        const bool ok = (ib < ni[k]) && (jb + c < nj[k]);
+                        const float2 f = ok ? fv[k][c] : make_float2(0.f, 0.f);
+                        const float2 a = hv[k][c];
+                        a0[k] = make_float2(fmaf(a.x, f.x, a0[k].x), fmaf(a.y, f.x, a0[k].y));
+                        a1[k] = make_float2(fmaf(a.x, f.y, a1[k].x), fmaf(a.y, f.y, a1[k].y));
                     }
             }
         }
-        float2* dst = B + 2 * pr * pslot + u * ld2 + v;
-        dst[0] = a0;
-        if (2 * pr + 1 < npath) dst[pslot] = a1;
+#pragma unroll
+        for (int k = 0; k < IT; ++k) {
+            if (w0 + k * T >= total) continue;
+            float2* dst = B + 2 * pr[k] * pslot + u[k] * ld2 + v[k];
+            dst[0] = a0[k];
+            if (2 * pr[k] + 1 < npath) dst[pslot] = a1[k];
+        }
     }
+}
+
+// 8-byte load through a buffer descriptor: 32-bit lane offset + wave-uniform offset, no 64-bit
+// address arithmetic per load.
+// Buffer descriptor over [base, base + bytes) from wave-uniform inputs, made provably uniform
+// (readfirstlane) so the compiler emits no waterfall loop around the loads.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base, int bytes) {
+    const unsigned long long a = reinterpret_cast<unsigned long long>(base);
+    const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(a));
+    const unsigned hi = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(a >> 32));
+    void* b = reinterpret_cast<void*>((static_cast<unsigned long long>(hi) << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(b, static_cast<short>(0),
+                                             __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+__device__ __forceinline__ float2 buf_load2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
 
 // s = 2 fold (j2 = j1 + 1, ~93 % of the alias box is significant, so dense): with nN2 = nN1 / 2
 // the four taps of (u, v) are rows u, u + nM2 and columns v (direct) and v + nN2 (the Hermitian
 // mirror conj(H[krm][nN2 - v]) for v > 0, H[kr][nN2] for v = 0); krm(u) = (nM1 - u) % nM1 and
 // krm(u + nM2) = nM2 - u.
-__device__ __forceinline__ void fold2_s2(const float2* H, int hld, int nM1, int nN1,
+// Each lane keeps one column v (its mirror column and sign are fixed) and walks the rows
+// (pair, u) of the batch in steps of rpp = T / nN2 (lanes beyond rpp * nN2 idle); the filter
+// taps come through a buffer descriptor with the row offsets as wave-uniform soffsets.
+__device__ __forceinline__ void fold2_s2(const float2* __restrict__ H, int hld, int nM1, int nN1,
                                          const float2* __restrict__ psi2, long long pstride,
-                                         int npair, int npath, float2* B, int pslot, int ld2,
-                                         int nM2, int nN2) {
-    const int items = nM2 * nN2;
-    const int total = npair * items;
-    const int T = blockDim.x;
-    const wstfft::FastDiv ditems(items), dn(nN2);
-    // two items per iteration: their 8 filter loads (L2) and 8 spectrum reads are in flight together
-    for (int w0 = threadIdx.x; w0 < total; w0 += 2 * T) {
-        float2 h[2][4], f[2][4];
-        int pr[2], u[2], v[2];
-        bool ok[2];
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int w = w0 + k * T;
-            ok[k] = w < total;
-            const int ww = ok[k] ? w : w0;
-            pr[k] = ditems.div(ww);
-            const int it = ww - pr[k] * items;
-            u[k] = dn.div(it);
-            v[k] = it - u[k] * nN2;
-            const float2* ps = psi2 + pr[k] * pstride;
-            const int r0 = u[k], r1 = u[k] + nM2;
-            const int m0 = r0 == 0 ? 0 : nM1 - r0, m1 = nM2 - r0;
-            const int cm = nN2 - v[k];
-            const bool v0 = v[k] == 0;
-            h[k][0] = H[r0 * hld + v[k]];
-            h[k][1] = H[v0 ? r0 * hld + nN2 : m0 * hld + cm];
-            h[k][2] = H[r1 * hld + v[k]];
-            h[k][3] = H[v0 ? r1 * hld + nN2 : m1 * hld + cm];
-            f[k][0] = ps[r0 * nN1 + v[k]];
-            f[k][1] = ps[r0 * nN1 + v[k] + nN2];
-            f[k][2] = ps[r1 * nN1 + v[k]];
-            f[k][3] = ps[r1 * nN1 + v[k] + nN2];
-            if (!v0) {
-                h[k][1].y = -h[k][1].y;
-                h[k][3].y = -h[k][3].y;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            if (!ok[k]) continue;
-            float2 a0, a1;
-            a0.x = fmaf(h[k][0].x, f[k][0].x, fmaf(h[k][1].x, f[k][1].x, fmaf(h[k][2].x, f[k][2].x, h[k][3].x * f[k][3].x)));
-            a0.y = fmaf(h[k][0].y, f[k][0].x, fmaf(h[k][1].y, f[k][1].x, fmaf(h[k][2].y, f[k][2].x, h[k][3].y * f[k][3].x)));
-            a1.x = fmaf(h[k][0].x, f[k][0].y, fmaf(h[k][1].x, f[k][1].y, fmaf(h[k][2].x, f[k][2].y, h[k][3].x * f[k][3].y)));
-            a1.y = fmaf(h[k][0].y, f[k][0].y, fmaf(h[k][1].y, f[k][1].y, fmaf(h[k][2].y, f[k][2].y, h[k][3].y * f[k][3].y)));
-            float2* dst = B + 2 * pr[k] * pslot + u[k] * ld2 + v[k];
-            dst[0] = a0;
-            if (2 * pr[k] + 1 < npath) dst[pslot] = a1;
-        }
+                                         int npair, int npath, float2* __restrict__ B, int pslot,
+                                         int ld2, int nM2, int nN2) {
+    const int rpp = blockDim.x / nN2;
+    const int t0 = threadIdx.x / nN2;
+    if (t0 >= rpp) return;
+    const int v = threadIdx.x - t0 * nN2;
+    const bool v0 = v == 0;
+    const int cB = v0 ? nN2 : nN2 - v;  // column of the two mirrored taps
+    const float sg = v0 ? 1.f : -1.f;   // their conjugation
+    const int hq = nM2 * hld;           // H offset of row u + nM2
+    const int fq = nM2 * nN1 * 8;       // filter byte offset of row u + nM2
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, static_cast<int>(npair * pstride * 8));
+    const wstfft::FastDiv dm(nM2);
+    const int rows = npair * nM2;
+    for (int pu = t0; pu < rows; pu += rpp) {
+        const int pr = dm.div(pu);
+        const int u = pu - pr * nM2;
+        const int hr = u * hld;
+        const int hm0 = v0 ? hr : (u == 0 ? 0 : (nM1 - u) * hld);
+        const int hm1 = v0 ? hr + hq : (nM2 - u) * hld;
+        float2 h[4];
+        h[0] = H[hr + v];
+        h[1] = H[hm0 + cB];
+        h[2] = H[hr + hq + v];
+        h[3] = H[hm1 + cB];
+        h[1].y *= sg;
+        h[3].y *= sg;
+        const int fo = (static_cast<int>(pr * pstride) + u * nN1 + v) * 8;
+        float2 f[4];
+        f[0] = buf_load2(rs, fo, 0);
+        f[1] = buf_load2(rs, fo, nN2 * 8);
+        f[2] = buf_load2(rs, fo, fq);
+        f[3] = buf_load2(rs, fo, fq + nN2 * 8);
+        float2 a0, a1;
+        a0.x = fmaf(h[0].x, f[0].x, fmaf(h[1].x, f[1].x, fmaf(h[2].x, f[2].x, h[3].x * f[3].x)));
+        a0.y = fmaf(h[0].y, f[0].x, fmaf(h[1].y, f[1].x, fmaf(h[2].y, f[2].x, h[3].y * f[3].x)));
+        a1.x = fmaf(h[0].x, f[0].y, fmaf(h[1].x, f[1].y, fmaf(h[2].x, f[2].y, h[3].x * f[3].y)));
+        a1.y = fmaf(h[0].y, f[0].y, fmaf(h[1].y, f[1].y, fmaf(h[2].y, f[2].y, h[3].y * f[3].y)));
+        float2* dst = B + 2 * pr * pslot + u * ld2 + v;
+        dst[0] = a0;
+        if (2 * pr + 1 < npath) dst[pslot] = a1;
     }
 }
 
