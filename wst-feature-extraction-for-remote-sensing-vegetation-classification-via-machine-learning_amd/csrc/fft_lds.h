@@ -218,16 +218,49 @@ WST_HD float2 cmul_tw(float2 a, float2 w, bool conj) {
 // Exact division by a runtime divisor d (1 <= d < 2^20) for 0 <= x < 2^31 as one mul-hi, one add
 // and one shift (round-up magic number, as in PyTorch's IntDivider); replaces the ~20-instruction
 // integer division the compiler emits for a runtime divisor in the per-unit index decode.
+// m = floor(2^32 (2^sh - d) / d) + 1 with 2^sh >= d; 2^32 (2^sh - d) < 2^52, exact in uint64.
+constexpr unsigned fastdiv_magic(int d, int sh) {
+    return static_cast<unsigned>(((1ull << 32) * ((1ull << sh) - static_cast<unsigned long long>(d))) /
+                                 static_cast<unsigned long long>(d)) + 1u;
+}
+constexpr int fastdiv_shift(int d) {
+    int sh = 0;
+    while ((1 << sh) < d) ++sh;
+    return sh;
+}
+// Device-side magics of every divisor up to kFastDivTab, built at compile time: a FastDiv built
+// in a kernel is then a clz plus one (uniform, scalar) table load instead of a double-precision
+// division (which the kernels' per-batch Lines / decode set-ups executed dozens of times per
+// workgroup).
+constexpr int kFastDivTab = 16384;
+struct FastDivTable {
+    unsigned m[kFastDivTab + 1];
+};
+constexpr FastDivTable make_fastdiv_table() {
+    FastDivTable t{};
+    for (int d = 1; d <= kFastDivTab; ++d) t.m[d] = fastdiv_magic(d, fastdiv_shift(d));
+    return t;
+}
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ static const FastDivTable kFastDivMagic = make_fastdiv_table();
+#endif
+
 struct FastDiv {
     unsigned m = 1;
     int sh = 0;
     WST_HD FastDiv() {}
     WST_HD explicit FastDiv(int d) {
-        sh = 0;
-        while ((1 << sh) < d) ++sh;
-        // floor(2^32 (2^sh - d) / d) + 1; the double quotient is exact to the floor for d < 2^20
-        m = static_cast<unsigned>(4294967296.0 * static_cast<double>((1 << sh) - d) /
-                                  static_cast<double>(d)) + 1u;
+#if defined(__HIP_DEVICE_COMPILE__)
+        sh = d > 1 ? 32 - __clz(d - 1) : 0;
+        // beyond the table (not met by the LDS-resident kernels): the double quotient is exact
+        // to the floor for d < 2^20
+        m = d <= kFastDivTab ? kFastDivMagic.m[d]
+                             : static_cast<unsigned>(4294967296.0 * static_cast<double>((1 << sh) - d) /
+                                                     static_cast<double>(d)) + 1u;
+#else
+        sh = fastdiv_shift(d);
+        m = fastdiv_magic(d, sh);
+#endif
     }
     WST_HD int div(int x) const {
 #if defined(__HIP_DEVICE_COMPILE__)
