@@ -849,6 +849,20 @@ __global__ void __launch_bounds__(1024) k_prep(DevParams p, LdsLayout lay,
 // every level-j1 size is in (prev_cap(CAP), CAP] and the order-2 paths are <= CAP / 2: the
 // kernel carries only those FFTs (code size stays well inside the instruction cache).
 constexpr int prev_cap(int c) { return c <= 12 ? 0 : c <= 24 ? 12 : c <= 48 ? 24 : 48; }
+// The level size of an SQ launch when its size class holds exactly one size of the family
+// (family 3: 96 / 48 / 24, family 5: 80 / 40 / 20, family 9: 72 / 36 / 18), else 0 (runtime).
+// With it every level size of the kernel is a compile-time constant: loop bounds, strides and
+// index decodes fold, the FFT-size dispatch disappears (geometry-specialised kernels).
+constexpr int unique_level(int fam, int cap) {
+    if (fam <= 0) return 0;
+    int found = 0, count = 0;
+    for (int n = fam; n <= cap; n *= 2)
+        if (n > prev_cap(cap)) {
+            found = n;
+            ++count;
+        }
+    return count == 1 ? found : 0;
+}
 
 // Minimum waves per SIMD for k_o1 per size class: the 96^2-class level runs 768-thread
 // workgroups, two per CU (LDS-bound), so it needs <= 80 VGPRs (6 waves per SIMD).
@@ -873,7 +887,9 @@ __global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevPara
     const int l1 = item - local * L;
     const long long img = img0 + local;
     const int PM = p.PM, PN = p.PN;
-    const int nM1 = PM >> j1, nN1 = PN >> j1, n1 = nM1 * nN1, ld1 = odd_ld(nN1);
+    constexpr int N1C = SQ ? unique_level(FM, MAXN) : 0;
+    const int nM1 = N1C ? N1C : PM >> j1, nN1 = N1C ? N1C : PN >> j1;
+    const int n1 = nM1 * nN1, ld1 = odd_ld(nN1);
     const bool do2 = (p.max_order >= 2) && (j1 < J - 1);
     float2* A = reinterpret_cast<float2*>(smem);
     float* S = reinterpret_cast<float*>(smem + lay.off_s);
@@ -951,7 +967,9 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
     const int l1 = item - local * L;
     const long long img = img0 + local;
     const int PM = p.PM, PN = p.PN;
-    const int nM1 = PM >> j1, nN1 = PN >> j1, n1 = nM1 * nN1;
+    constexpr int N1C = (SQ && !HG) ? unique_level(FM, MAXN) : 0;
+    const int nM1 = N1C ? N1C : PM >> j1, nN1 = N1C ? N1C : PN >> j1;
+    const int n1 = nM1 * nN1;
     const int hld = (nN1 >> 1) + 1;
     const float2* Hg = hexp + static_cast<long long>(item) * nM1 * hld;
     const float2* H = HG ? Hg : reinterpret_cast<const float2*>(smem);
@@ -981,8 +999,9 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
     // 2. order-2 paths in batches: Hermitian fold -> |ifft| -> S2 low-pass
     const int kbase = p.o2_base[j1 * L + l1];
     const int nq = (L + 1) >> 1;
-    for (int j2 = j2first; j2 < J; ++j2) {
-        const int nM2 = PM >> j2, nN2 = PN >> j2, ld2 = odd_ld(nN2);
+    // every batch of paths of level j2 (sizes nM2 x nN2)
+    auto level = [&](int j2, int nM2, int nN2) __attribute__((always_inline)) {
+        const int ld2 = odd_ld(nN2);
         const int pslot = nM2 * ld2;
         const int s2 = 1 << (j2 - j1);
         int pb = lay.bcap / pslot;                 // paths per batch (multiple of 2)
@@ -1027,6 +1046,17 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
             // no barrier here: the next batch's fold writes B only, and S is rewritten only after
             // that batch's transform barriers (emit above reads S alone)
         }
+    };
+    if constexpr (N1C > 0) {
+        // compile-time level sizes N1C / 2^k (the paths of an SQ launch start at j2 = j1 + 1)
+        wstfft::static_for<1, 8>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int NN2 = N1C >> k;
+            if constexpr ((NN2 << k) == N1C && NN2 >= 1)
+                if (j1 + k < J) level(j1 + k, NN2, NN2);
+        });
+    } else {
+        for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2);
     }
 }
 
