@@ -313,6 +313,90 @@ __device__ __forceinline__ void lds_lowpass(float2* U, int nb, int bs, int rows,
 
 constexpr int kLpOM = 8;  // row stride of the GM tap matrices = largest oM of the fused path
 
+// Separable phi low-pass of one (rows x cols) real array (U[p][q].x, row stride ld) at the kept
+// output points through the level's tap matrices (physical order, unpad and decimation folded in;
+// host: lpt):  S[a][c] = sum_p GM[p][a] sum_q GN[q][c] U[p][q], oM, oN <= oms (4 or 8).  The
+// row partials T[p][c] are parked in the free .y slots of row p.  One float4 load brings four
+// taps (lds_lowpass: a table load and a permutation lookup per tap).  Ends with a barrier.
+template <int QC, int PC>
+__device__ __forceinline__ void lds_lowpass_taps(float2* U, int rows, int cols, int ld,
+                                                 const float* GM, const float* GN, int oms, int oM,
+                                                 int oN, float* S) {
+    const int T = blockDim.x;
+    const bool w8 = oms > 4;
+    // 1. T[p][c] = sum_q GN[q][c] U[p][q]: QC lanes per row
+    for (int w = threadIdx.x; w < rows * QC; w += T) {
+        const int qc = w & (QC - 1);
+        const int p = w / QC;
+        float2* row = U + p * ld;
+        float acc[kLpOM];
+#pragma unroll
+        for (int c = 0; c < kLpOM; ++c) acc[c] = 0.f;
+        for (int q = qc; q < cols; q += QC) {
+            const float x = row[q].x;
+            const float4 g0 = *reinterpret_cast<const float4*>(GN + q * oms);
+            acc[0] = fmaf(g0.x, x, acc[0]);
+            acc[1] = fmaf(g0.y, x, acc[1]);
+            acc[2] = fmaf(g0.z, x, acc[2]);
+            acc[3] = fmaf(g0.w, x, acc[3]);
+            if (w8) {
+                const float4 g1 = *reinterpret_cast<const float4*>(GN + q * oms + 4);
+                acc[4] = fmaf(g1.x, x, acc[4]);
+                acc[5] = fmaf(g1.y, x, acc[5]);
+                acc[6] = fmaf(g1.z, x, acc[6]);
+                acc[7] = fmaf(g1.w, x, acc[7]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < kLpOM; ++c) {
+            if (c >= 4 && !w8) break;
+#pragma unroll
+            for (int off = QC / 2; off >= 1; off >>= 1) acc[c] += __shfl_xor(acc[c], off, 64);
+        }
+        if (qc == 0) {
+#pragma unroll
+            for (int c = 0; c < kLpOM; ++c)
+                if (c < oN) row[c].y = acc[c];
+        }
+    }
+    __syncthreads();
+    // 2. S[a][c] = sum_p GM[p][a] T[p][c]: PC lanes per output column c
+    for (int w = threadIdx.x; w < oN * PC; w += T) {
+        const int pc = w & (PC - 1);
+        const int c = w / PC;
+        float acc[kLpOM];
+#pragma unroll
+        for (int a = 0; a < kLpOM; ++a) acc[a] = 0.f;
+        for (int p = pc; p < rows; p += PC) {
+            const float t = U[p * ld + c].y;
+            const float4 g0 = *reinterpret_cast<const float4*>(GM + p * oms);
+            acc[0] = fmaf(g0.x, t, acc[0]);
+            acc[1] = fmaf(g0.y, t, acc[1]);
+            acc[2] = fmaf(g0.z, t, acc[2]);
+            acc[3] = fmaf(g0.w, t, acc[3]);
+            if (w8) {
+                const float4 g1 = *reinterpret_cast<const float4*>(GM + p * oms + 4);
+                acc[4] = fmaf(g1.x, t, acc[4]);
+                acc[5] = fmaf(g1.y, t, acc[5]);
+                acc[6] = fmaf(g1.z, t, acc[6]);
+                acc[7] = fmaf(g1.w, t, acc[7]);
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < kLpOM; ++a) {
+            if (a >= 4 && !w8) break;
+#pragma unroll
+            for (int off = PC / 2; off >= 1; off >>= 1) acc[a] += __shfl_xor(acc[a], off, 64);
+        }
+        if (pc == 0) {
+#pragma unroll
+            for (int a = 0; a < kLpOM; ++a)
+                if (a < oM) S[a * oN + c] = acc[a];
+        }
+    }
+    __syncthreads();
+}
+
 // Inverse column pass (in place, natural -> digit-reversed rows) of nb (NN x cols) arrays U_b,
 // fused with |.| * scale and the phi low-pass (unpad and decimation folded
 // into the tap matrices GM (physical row p -> kept output row a) and GN (column q -> output c)):
@@ -931,8 +1015,11 @@ __global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevPara
     // 3. S1 at level j1, decimation 2^(J-j1)
     const int n1idx = j1 * L + l1;
     if (!(dbg & 2)) {
-        lds_lowpass(A, 1, 0, nM1, nN1, ld1, tb.lpM(j1), tb.lpN(j1), tb.pmM(j1), tb.pmN(j1),
-                    1 << (J - j1), p.oM, p.oN, S);
+        if constexpr (SQ)
+            lds_lowpass_taps<8, 16>(A, nM1, nN1, ld1, tb.gM(j1), tb.gN(j1), lay.oms, p.oM, p.oN, S);
+        else
+            lds_lowpass(A, 1, 0, nM1, nN1, ld1, tb.lpM(j1), tb.lpN(j1), tb.pmM(j1), tb.pmN(j1),
+                        1 << (J - j1), p.oM, p.oN, S);
         emit(S, 1, 1 + n1idx, img, p.K, p.oM, p.oN, out, pooled);
     }
     if (!do2) return;

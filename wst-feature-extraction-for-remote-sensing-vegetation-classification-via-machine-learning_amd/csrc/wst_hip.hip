@@ -670,8 +670,14 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
             (plan->fam_m == 3 || plan->fam_m == 5 || plan->fam_m == 9))
             plan->o1_threads[j1] = 768;
         plan->o2_threads[j1] = default_threads(n1);
-        plan->o1_lds[j1] = layout(plan->o1_lay[j1], static_cast<size_t>(nM1) * odd_ld(nN1) * sizeof(float2),
-                                  0, t, Blocks{j1, j1, !plan->sq}, j1, j1, omn);
+        // SQ kernels: the S1 low-pass runs on the level's tap matrices (lds_lowpass_taps) instead
+        // of the 1-D taps and permutations
+        if (plan->sq)
+            plan->o1_lds[j1] = layout(plan->o1_lay[j1], static_cast<size_t>(nM1) * odd_ld(nN1) * sizeof(float2),
+                                      0, t, Blocks{j1, j1, false}, 1, 0, omn, Blocks{j1, j1, false}, oms);
+        else
+            plan->o1_lds[j1] = layout(plan->o1_lay[j1], static_cast<size_t>(nM1) * odd_ld(nN1) * sizeof(float2),
+                                      0, t, Blocks{j1, j1, true}, j1, j1, omn);
         if (plan->o1_lds[j1] > static_cast<size_t>(kMaxLds)) return too_big("k_o1", j1);
         if (!do2) continue;
         if (nM1 % 2 != 0 || nN1 % 2 != 0)
