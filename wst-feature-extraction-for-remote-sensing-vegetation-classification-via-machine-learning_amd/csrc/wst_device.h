@@ -42,9 +42,6 @@ __device__ unsigned long long wst_stamps[kStampBlocks * kStampSlots];
 #else
 #define WST_STAMP(ctr) do {} while (0)
 #endif
-#ifndef WST_FOLD_IT
-#define WST_FOLD_IT 1  // box-sparse order-2 fold: items folded together per thread
-#endif
 
 namespace wstdev {
 
@@ -722,96 +719,6 @@ __device__ __forceinline__ void fold1_any(int s1, const float2* X, const float* 
     else fold1<0>(X, psi0, PN, A, ld1, nM1, nN1, s1);
 }
 
-// Order-2 Hermitian fold of npair filter pairs (2 paths each) into B:
-//   B_b[u][v] = sum_{i,j < s} U1hat[u + i nM2][v + j nN2] * psi_b[...]
-// U1hat is read from the half spectrum H (nM1 x hld, columns 0..nN1/2):
-//   U1hat[kr][kc] = kc <= nN1/2 ? H[kr][kc] : conj(H[(nM1 - kr) % nM1][nN1 - kc]).
-// Box-sparse: only the aliases i in [i0, i0 + ni) (mod s) of row u and j in [j0, j0 + nj) of
-// column v are summed, where the pair's alias boxes (host: box_bins) cover every bin at which
-// either filter exceeds kBoxThreshold * its maximum; the dropped terms are below that bound.
-template <int S>
-__device__ __forceinline__ void fold2(const float2* H, int hld, int nM1, int nN1,
-                                      const float2* __restrict__ psi2, long long pstride,
-                                      int npair, int npath, float2* B, int pslot, int ld2, int nM2,
-                                      int nN2, int s_rt, const int* __restrict__ box, int bstride) {
-    const int s = (S > 0) ? S : s_rt;
-    const int smask = s - 1;
-    const int half = nN1 >> 1;
-    const int items = nM2 * nN2;
-    const int total = npair * items;
-    const wstfft::FastDiv ditems(items), dn(nN2);
-    // IT items per thread are folded together and their taps gathered in blocks of BC column
-    // aliases per item, all loads of a block issued before the first is consumed (a tap outside
-    // an item's box re-reads its box's last row / column with weight 0), so one L2 round trip
-    // serves IT * BC taps.
-    constexpr int IT = WST_FOLD_IT, BC = 4;
-    const int T = blockDim.x;
-    for (int w0 = threadIdx.x; w0 < total; w0 += IT * T) {
-        int pr[IT], u[IT], v[IT], i0[IT], ni[IT], j0[IT], nj[IT];
-        int nimax = 0, njmax = 0;
-#pragma unroll
-        for (int k = 0; k < IT; ++k) {
-            const int w = w0 + k * T;
-            const int ww = w < total ? w : w0;
-            pr[k] = ditems.div(ww);
-            const int it = ww - pr[k] * items;
-            u[k] = dn.div(it);
-            v[k] = it - u[k] * nN2;
-            const int* bx = box + pr[k] * bstride;
-            const int rb = bx[u[k]], cb = bx[nM2 + v[k]];
-            i0[k] = rb & 255;
-            j0[k] = cb & 255;
-            ni[k] = w < total ? rb >> 8 : 0;
-            nj[k] = cb >> 8;
-            nimax = max(nimax, ni[k]);
-            njmax = max(njmax, nj[k]);
-        }
-        float2 a0[IT], a1[IT];
-#pragma unroll
-        for (int k = 0; k < IT; ++k) a0[k] = a1[k] = make_float2(0.f, 0.f);
-        for (int ib = 0; ib < nimax; ++ib) {
-            for (int jb = 0; jb < njmax; jb += BC) {
-                float2 hv[IT][BC], fv[IT][BC];
-#pragma unroll
-                for (int k = 0; k < IT; ++k) {
-                    // (i0 + min(ib, ni - 1)) & smask stays a valid alias even for ni = 0
-                    const int kr = u[k] + ((i0[k] + min(ib, ni[k] - 1)) & smask) * nM2;
-                    const int krm = kr == 0 ? 0 : nM1 - kr;
-                    const float2* frow = psi2 + pr[k] * pstride + kr * nN1;
-                    const float2* hrow = H + kr * hld;
-                    const float2* hmir = H + krm * hld + nN1;
-#pragma unroll
-                    for (int c = 0; c < BC; ++c) {
-                        const int kc = v[k] + ((j0[k] + min(jb + c, nj[k] - 1)) & smask) * nN2;
-                        const bool mir = kc > half;
-                        float2 a = mir ? hmir[-kc] : hrow[kc];
-                        a.y = mir ? -a.y : a.y;
-                        hv[k][c] = a;
-                        fv[k][c] = frow[kc];
-                    }
-                }
-#pragma unroll
-                for (int k = 0; k < IT; ++k)
-#pragma unroll
-                    for (int c = 0; c < BC; ++c) {
-                        const bool ok = (ib < ni[k]) && (jb + c < nj[k]);
-                        const float2 f = ok ? fv[k][c] : make_float2(0.f, 0.f);
-                        const float2 a = hv[k][c];
-                        a0[k] = make_float2(fmaf(a.x, f.x, a0[k].x), fmaf(a.y, f.x, a0[k].y));
-                        a1[k] = make_float2(fmaf(a.x, f.y, a1[k].x), fmaf(a.y, f.y, a1[k].y));
-                    }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < IT; ++k) {
-            if (w0 + k * T >= total) continue;
-            float2* dst = B + 2 * pr[k] * pslot + u[k] * ld2 + v[k];
-            dst[0] = a0[k];
-            if (2 * pr[k] + 1 < npath) dst[pslot] = a1[k];
-        }
-    }
-}
-
 // 8-byte load through a buffer descriptor: 32-bit lane offset + wave-uniform offset, no 64-bit
 // address arithmetic per load.
 // Buffer descriptor over [base, base + bytes) from wave-uniform inputs, made provably uniform
@@ -827,6 +734,78 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
 
 __device__ __forceinline__ float2 buf_load2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
     return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+
+// Order-2 Hermitian fold of npair filter pairs (2 paths each) into B:
+//   B_b[u][v] = sum_{i,j < s} U1hat[u + i nM2][v + j nN2] * psi_b[...]
+// U1hat is read from the half spectrum H (nM1 x hld, columns 0..nN1/2):
+//   U1hat[kr][kc] = kc <= nN1/2 ? H[kr][kc] : conj(H[(nM1 - kr) % nM1][nN1 - kc]).
+// Box-sparse: only the aliases i in [i0, i0 + ni) (mod s) of row u and j in [j0, j0 + nj) of
+// column v are summed, where the pair's alias boxes (host: box_bins) cover every bin at which
+// either filter exceeds kBoxThreshold * its maximum; the dropped terms are below that bound.
+// Column taps go in blocks of four, set up once per block (H column, mirror, sign and a zero
+// weight past the box -- the out-of-box alias stays a valid address), then the block walks the
+// box rows: per tap one LDS read, one buffer load (32-bit offsets) and the products.
+template <int S>
+__device__ __forceinline__ void fold2(const float2* __restrict__ H, int hld, int nM1, int nN1,
+                                      const float2* __restrict__ psi2, long long pstride,
+                                      int npair, int npath, float2* __restrict__ B, int pslot,
+                                      int ld2, int nM2, int nN2, int s_rt,
+                                      const int* __restrict__ box, int bstride) {
+    const int s = (S > 0) ? S : s_rt;
+    const int smask = s - 1;
+    const int half = nN1 >> 1;
+    const int items = nM2 * nN2;
+    const int total = npair * items;
+    const wstfft::FastDiv ditems(items), dn(nN2);
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, static_cast<int>(npair * pstride * 8));
+    for (int w = threadIdx.x; w < total; w += blockDim.x) {
+        const int pr = ditems.div(w);
+        const int it = w - pr * items;
+        const int u = dn.div(it), v = it - u * nN2;
+        const int* bx = box + pr * bstride;
+        const int rb = bx[u], cb = bx[nM2 + v];
+        const int i0 = rb & 255, ni = rb >> 8, j0 = cb & 255, nj = cb >> 8;
+        const int fpr = static_cast<int>(pr * pstride);
+        float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+        for (int jb = 0; jb < nj; jb += 4) {
+            int hc[4], fc[4];
+            bool mir[4];
+            float wx[4], wy[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const bool ok = jb + c < nj;
+                const int kc = v + ((j0 + jb + c) & smask) * nN2;
+                mir[c] = kc > half;
+                hc[c] = mir[c] ? nN1 - kc : kc;
+                fc[c] = kc * 8;
+                wx[c] = ok ? 1.f : 0.f;
+                wy[c] = ok ? (mir[c] ? -1.f : 1.f) : 0.f;
+            }
+            for (int i = 0; i < ni; ++i) {
+                const int kr = u + ((i0 + i) & smask) * nM2;
+                const int krm = kr == 0 ? 0 : nM1 - kr;
+                const float2* hd = H + kr * hld;
+                const float2* hm = H + krm * hld;
+                const int fo = (fpr + kr * nN1) * 8;
+                float2 hv[4], fv[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    hv[c] = (mir[c] ? hm : hd)[hc[c]];
+                    fv[c] = buf_load2(rs, fo + fc[c], 0);
+                }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float hx = hv[c].x * wx[c], hy = hv[c].y * wy[c];
+                    a0 = make_float2(fmaf(hx, fv[c].x, a0.x), fmaf(hy, fv[c].x, a0.y));
+                    a1 = make_float2(fmaf(hx, fv[c].y, a1.x), fmaf(hy, fv[c].y, a1.y));
+                }
+            }
+        }
+        float2* dst = B + 2 * pr * pslot + u * ld2 + v;
+        dst[0] = a0;
+        if (2 * pr + 1 < npath) dst[pslot] = a1;
+    }
 }
 
 // s = 2 fold (j2 = j1 + 1, ~93 % of the alias box is significant, so dense): with nN2 = nN1 / 2
