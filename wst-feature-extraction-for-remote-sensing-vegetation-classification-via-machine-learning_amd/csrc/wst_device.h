@@ -880,13 +880,28 @@ __device__ __forceinline__ int xcd_item(int total) {
 // ------------------------------------------------------------------------------------------
 // k_prep: one workgroup per plane
 // ------------------------------------------------------------------------------------------
-template <int FM, int FN>
-__global__ void __launch_bounds__(1024) k_prep(DevParams p, LdsLayout lay,
-                                               const float* __restrict__ in, long long img0,
-                                               float2* __restrict__ xhat, float* __restrict__ out,
-                                               int pooled) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int PM = p.PM, PN = p.PN, n = PM * PN, ld = odd_ld(PN);
+constexpr int prev_cap(int c) { return c <= 12 ? 0 : c <= 24 ? 12 : c <= 48 ? 24 : 48; }
+// The level size of an SQ launch when its size class holds exactly one size of the family
+// (family 3: 96 / 48 / 24, family 5: 80 / 40 / 20, family 9: 72 / 36 / 18), else 0 (runtime).
+// With it every level size of the kernel is a compile-time constant: loop bounds, strides and
+// index decodes fold, the FFT-size dispatch disappears (geometry-specialised kernels).
+constexpr int unique_level(int fam, int cap) {
+    if (fam <= 0) return 0;
+    int found = 0, count = 0;
+    for (int n = fam; n <= cap; n *= 2)
+        if (n > prev_cap(cap)) {
+            found = n;
+            ++count;
+        }
+    return count == 1 ? found : 0;
+}
+
+template <int FM, int FN, int PC>
+__device__ __forceinline__ void prep_body(unsigned char* smem, const DevParams& p, const LdsLayout& lay,
+                                          const float* __restrict__ in, long long img0,
+                                          float2* __restrict__ xhat, float* __restrict__ out,
+                                          int pooled) {
+    const int PM = PC ? PC : p.PM, PN = PC ? PC : p.PN, n = PM * PN, ld = odd_ld(PN);
     float2* A = reinterpret_cast<float2*>(smem);
     float* S = reinterpret_cast<float*>(smem + lay.off_s);
     float* red = reinterpret_cast<float*>(smem + lay.off_red);
@@ -922,26 +937,28 @@ __global__ void __launch_bounds__(1024) k_prep(DevParams p, LdsLayout lay,
     for (GridIter it(PN); it.u < PM; it.next()) dst[it.u * PN + it.v] = A[it.u * ld + it.v];
 }
 
+// One workgroup per plane.  Square planes at the family's single 96^2-class size (unique_level)
+// run with compile-time sizes.
+template <int FM, int FN>
+__global__ void __launch_bounds__(1024) k_prep(DevParams p, LdsLayout lay,
+                                               const float* __restrict__ in, long long img0,
+                                               float2* __restrict__ xhat, float* __restrict__ out,
+                                               int pooled) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int PC = FM == FN ? unique_level(FM, 136) : 0;
+    if constexpr (PC > 0) {
+        if (p.PM == PC && p.PN == PC) {
+            prep_body<FM, FN, PC>(smem, p, lay, in, img0, xhat, out, pooled);
+            return;
+        }
+    }
+    prep_body<FM, FN, 0>(smem, p, lay, in, img0, xhat, out, pooled);
+}
+
 // Size classes of the k_o1 / k_o2 instantiations: CAP = largest level size of a launch
 // (max(PM, PN) >> j1).  SQ = 1: square plane whose order-2 low-pass fuses (fused_lowpass_ok), so
 // every level-j1 size is in (prev_cap(CAP), CAP] and the order-2 paths are <= CAP / 2: the
 // kernel carries only those FFTs (code size stays well inside the instruction cache).
-constexpr int prev_cap(int c) { return c <= 12 ? 0 : c <= 24 ? 12 : c <= 48 ? 24 : 48; }
-// The level size of an SQ launch when its size class holds exactly one size of the family
-// (family 3: 96 / 48 / 24, family 5: 80 / 40 / 20, family 9: 72 / 36 / 18), else 0 (runtime).
-// With it every level size of the kernel is a compile-time constant: loop bounds, strides and
-// index decodes fold, the FFT-size dispatch disappears (geometry-specialised kernels).
-constexpr int unique_level(int fam, int cap) {
-    if (fam <= 0) return 0;
-    int found = 0, count = 0;
-    for (int n = fam; n <= cap; n *= 2)
-        if (n > prev_cap(cap)) {
-            found = n;
-            ++count;
-        }
-    return count == 1 ? found : 0;
-}
-
 // Minimum waves per SIMD for k_o1 per size class: the 96^2-class level runs 768-thread
 // workgroups, two per CU (LDS-bound), so it needs <= 80 VGPRs (6 waves per SIMD).
 // (families 3, 5, 9 square: the others' FFT sizes spill at that budget and keep 512 threads;
