@@ -4,10 +4,11 @@ import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch, wst_amd  # noqa: F401
 from wst_amd import _lib
-B, J = 3072, 4
-x = torch.from_numpy(np.random.default_rng(1).integers(0, 256, (B, 64, 64), dtype=np.uint8).astype(np.float32) / 255).cuda()
-plan = _lib.Plan(64, 64, J, 8)
-out = torch.empty((B, plan.K, 4, 4), device="cuda")
+# geometry: env WST_KM_GEOM="planes,M,J" (default the c2 step: 3072 planes of 64^2, J=4)
+B, M, J = (int(v) for v in os.environ.get("WST_KM_GEOM", "3072,64,4").split(","))
+x = torch.from_numpy(np.random.default_rng(1).integers(0, 256, (B, M, M), dtype=np.uint8).astype(np.float32) / 255).cuda()
+plan = _lib.Plan(M, M, J, 8)
+out = torch.empty((B, plan.K, plan.Mo, plan.No), device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 nslot = 1 + 2 * J
 for chunk in [int(a) for a in sys.argv[1:]] or [2048]:

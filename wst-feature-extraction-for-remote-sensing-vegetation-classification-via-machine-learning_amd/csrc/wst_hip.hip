@@ -81,6 +81,15 @@ size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 // workgroups per CU at 96^2, smaller groups for the decimated levels)
 int default_threads(size_t n) { return n >= 8192 ? 512 : n >= 2048 ? 256 : n >= 512 ? 128 : 64; }
 
+// Workgroup size so that the workgroups LDS lets share a CU carry at least 1024 threads (16 waves):
+// a kernel held to one or a few workgroups per CU by its LDS otherwise runs at 2-3 waves per SIMD
+// (P = 136 planes: 512 -> 1024 threads, -24 % in k_o2; P = 72: 256 -> 512, -10 % overall).
+int fill_cu(int threads, size_t lds) {
+    const size_t wgs = std::max<size_t>(1, static_cast<size_t>(160 * 1024) / std::max<size_t>(lds, 1));
+    while (threads < 1024 && wgs * static_cast<size_t>(threads) < 1024) threads *= 2;
+    return threads;
+}
+
 // "t0,t1,..." tuning override of per-j1 thread counts
 void threads_override(const char* env, std::vector<int>& v) {
     const char* s = std::getenv(env);
@@ -712,6 +721,11 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
                          plan->cap[j1], plan->o1_threads[j1], plan->o1_lds[j1], plan->o2_threads[j1],
                          plan->o2_lds[j1]);
     }
+    for (int j1 = plan->rb; j1 < J; ++j1) {
+        plan->o1_threads[j1] = fill_cu(plan->o1_threads[j1], plan->o1_lds[j1]);
+        if (plan->o2_lds[j1] > 0) plan->o2_threads[j1] = fill_cu(plan->o2_threads[j1], plan->o2_lds[j1]);
+    }
+    if (plan->rb == 0) plan->prep_threads = fill_cu(static_cast<int>(plan->prep_threads), plan->prep_lds);
     threads_override("WST_O1_THREADS", plan->o1_threads);
     threads_override("WST_O2_THREADS", plan->o2_threads);
     WST_HIP_CHECK(plan->ops->set_attrs());
