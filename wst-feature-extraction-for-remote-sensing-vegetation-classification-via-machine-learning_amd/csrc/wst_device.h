@@ -42,6 +42,9 @@ __device__ unsigned long long wst_stamps[kStampBlocks * kStampSlots];
 #else
 #define WST_STAMP(ctr) do {} while (0)
 #endif
+#ifndef WST_LP_TILED
+#define WST_LP_TILED 1  // register-tiled separable low-pass for outputs wider than 8 (lds_lowpass)
+#endif
 
 namespace wstdev {
 
@@ -299,13 +302,113 @@ __device__ __forceinline__ void lds_lowpass_t(float2* U, int nb, int bs, int row
     __syncthreads();
 }
 
+// Register-tiled form for large outputs (oN > 8, e.g. 32 x 32 maps of 128^2 planes at J = 2): a
+// step-1 thread owns RP rows x OW output columns (each tap read once for RP rows), a step-2 thread
+// owns AP x CW outputs (taps and row partials read once per p for the whole tile); QC / PC lanes
+// split the reduction index.  Out-of-range tile rows / columns re-read the last valid one and are
+// not stored (the tap index stays inside the doubled tables: s * oN <= cols).
+template <int RP, int OW, int QC, int AP, int CW, int PC>
+__device__ __forceinline__ void lds_lowpass_tiled(float2* U, int nb, int bs, int rows, int cols,
+                                                  int ld, const float* hM2, const float* hN2,
+                                                  const int* permM, const int* permN, int s, int oM,
+                                                  int oN, float* S) {
+    const int T = blockDim.x;
+    const int npb = (rows + RP - 1) / RP, ncb = (oN + OW - 1) / OW;
+    const wstfft::FastDiv dcb(ncb), dpb(npb);
+    for (int w = threadIdx.x; w < nb * npb * ncb * QC; w += T) {
+        const int qc = w & (QC - 1);
+        int t = w / QC;
+        const int t1 = dcb.div(t);
+        const int cb = t - t1 * ncb;
+        const int b = dpb.div(t1);
+        const int p0 = (t1 - b * npb) * RP, c0 = cb * OW;
+        float2* base = U + b * bs;
+        float acc[RP][OW];
+#pragma unroll
+        for (int r = 0; r < RP; ++r)
+#pragma unroll
+            for (int c = 0; c < OW; ++c) acc[r][c] = 0.f;
+        for (int q = qc; q < cols; q += QC) {
+            const float* hq = hN2 + cols + s * (c0 + 1) - (permN ? permN[q] : q);
+            float tap[OW];
+#pragma unroll
+            for (int c = 0; c < OW; ++c) tap[c] = hq[s * min(c, oN - 1 - c0)];
+#pragma unroll
+            for (int r = 0; r < RP; ++r) {
+                const float x = base[min(p0 + r, rows - 1) * ld + q].x;
+#pragma unroll
+                for (int c = 0; c < OW; ++c) acc[r][c] = fmaf(x, tap[c], acc[r][c]);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RP; ++r)
+#pragma unroll
+            for (int c = 0; c < OW; ++c)
+#pragma unroll
+                for (int off = QC / 2; off >= 1; off >>= 1) acc[r][c] += __shfl_xor(acc[r][c], off, 64);
+        if (qc == 0) {
+#pragma unroll
+            for (int r = 0; r < RP; ++r)
+#pragma unroll
+                for (int c = 0; c < OW; ++c)
+                    if (p0 + r < rows && c0 + c < oN) base[(p0 + r) * ld + c0 + c].y = acc[r][c];
+        }
+    }
+    __syncthreads();
+    const int nab = (oM + AP - 1) / AP, ncw = (oN + CW - 1) / CW;
+    const wstfft::FastDiv dcw(ncw), dab(nab);
+    for (int w = threadIdx.x; w < nb * nab * ncw * PC; w += T) {
+        const int pc = w & (PC - 1);
+        int t = w / PC;
+        const int t1 = dcw.div(t);
+        const int cw = t - t1 * ncw;
+        const int b = dab.div(t1);
+        const int a0 = (t1 - b * nab) * AP, c0 = cw * CW;
+        const float2* base = U + b * bs;
+        float acc[AP][CW];
+#pragma unroll
+        for (int a = 0; a < AP; ++a)
+#pragma unroll
+            for (int c = 0; c < CW; ++c) acc[a][c] = 0.f;
+        for (int p = pc; p < rows; p += PC) {
+            const float* hp = hM2 + rows + s * (a0 + 1) - (permM ? permM[p] : p);
+            float tap[AP], tv[CW];
+#pragma unroll
+            for (int a = 0; a < AP; ++a) tap[a] = hp[s * min(a, oM - 1 - a0)];
+#pragma unroll
+            for (int c = 0; c < CW; ++c) tv[c] = base[p * ld + min(c0 + c, oN - 1)].y;
+#pragma unroll
+            for (int a = 0; a < AP; ++a)
+#pragma unroll
+                for (int c = 0; c < CW; ++c) acc[a][c] = fmaf(tap[a], tv[c], acc[a][c]);
+        }
+#pragma unroll
+        for (int a = 0; a < AP; ++a)
+#pragma unroll
+            for (int c = 0; c < CW; ++c)
+#pragma unroll
+                for (int off = PC / 2; off >= 1; off >>= 1) acc[a][c] += __shfl_xor(acc[a][c], off, 64);
+        if (pc == 0) {
+#pragma unroll
+            for (int a = 0; a < AP; ++a)
+#pragma unroll
+                for (int c = 0; c < CW; ++c)
+                    if (a0 + a < oM && c0 + c < oN) S[(b * oM + a0 + a) * oN + c0 + c] = acc[a][c];
+        }
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ void lds_lowpass(float2* U, int nb, int bs, int rows, int cols, int ld,
                                             const float* hM2, const float* hN2, const int* permM,
                                             const int* permN, int s, int oM, int oN, float* S) {
     if (oN <= 4)
         lds_lowpass_t<4, 8, 16>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, S);
-    else
+    else if (oN <= 8 || !WST_LP_TILED)
         lds_lowpass_t<8, 8, 16>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, S);
+    else
+        lds_lowpass_tiled<4, 8, 8, 4, 4, 8>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s,
+                                             oM, oN, S);
 }
 
 constexpr int kLpOM = 8;  // row stride of the GM tap matrices = largest oM of the fused path
