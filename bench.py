@@ -51,6 +51,11 @@ CONFIGS = {
     "c5": dict(workload="c5: 64 x 256x256 4-band patches, Scattering2D J=6 L=12 order-2 (per GPU; "
                         "384^2 and 192^2 levels HBM-staged)",
                C=4, M=256, N=256, J=6, L=12, batch=64),
+    # the geometry the reference's experiments were run at (128x128 RGB
+    # images, J=2, L=8: train_and_save_model.py:352-359 on experiment_report image_shape)
+    "f3": dict(workload="f3: 256 x 128x128 RGB patches, Scattering2D J=2 L=8 order-2 (the reference's "
+                        "experiment geometry; P = 136)",
+               C=3, M=128, N=128, J=2, L=8, batch=256),
 }
 
 
