@@ -1160,11 +1160,14 @@ constexpr int o2_min_waves(int cap) { return cap == 48 ? 6 : cap == 24 ? 5 : 1; 
 // HG = 1: the level-j1 spectrum is a big (HBM-staged, wst_staged.h) level: `hexp` holds the
 // fully transformed half spectra in natural order, the fold reads them from HBM (no LDS copy,
 // no column FFT) and the paths start at j2first (the first LDS-resident level).
-template <int FM, int FN, int MAXN, int SQ, int HG = 0>
-__global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, LdsLayout lay, int j1, int nimg,
-                                             long long img0, const float2* __restrict__ hexp,
-                                             float* __restrict__ out, int pooled, int j2first) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// k_o2 body; OC > 0: the output maps are OC x OC (compile-time; the common 4 x 4 of the headline)
+template <int FM, int FN, int MAXN, int SQ, int HG, int OC>
+__device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& p,
+                                          const LdsLayout& lay, int j1, int nimg, long long img0,
+                                          const float2* __restrict__ hexp, float* __restrict__ out,
+                                          int pooled, int j2first) {
+    const int oM = OC ? OC : p.oM, oN = OC ? OC : p.oN;
+    const int oms = OC ? 4 : lay.oms;
     const int J = p.J, L = p.L;
     const int item = xcd_item(nimg * L);
     const int local = item / L;
@@ -1229,13 +1232,13 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
                         B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, nN2, tb.twN(j2), id);
                 WST_STAMP(sctr);
                 const int k0 = kbase + (j2 - j1 - 1) * L + l2a;
-                float* outd = pooled ? nullptr : out + (img * p.K + k0) * (p.oM * p.oN);
+                float* outd = pooled ? nullptr : out + (img * p.K + k0) * (oM * oN);
                 if (!(dbg & 64))
                     family_cols_modlp<FM, 0, PHI>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
-                                                       tb.gM(j2), tb.gN(j2), lay.oms, p.oM, p.oN,
+                                                       tb.gM(j2), tb.gN(j2), oms, oM, oN,
                                                        scale2, S, outd);
                 WST_STAMP(sctr);
-                if (!outd) emit(S, npath, k0, img, p.K, p.oM, p.oN, out, pooled);
+                if (!outd) emit(S, npath, k0, img, p.K, oM, oN, out, pooled);
             } else {
                 EpiModulus mod2{scale2, 0.f};
                 if (!(dbg & 16))
@@ -1243,8 +1246,8 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
                                                          tb.twN(j2), mod2);
                 if (!(dbg & 64)) {
                     lds_lowpass(B, npath, pslot, nM2, nN2, ld2, tb.lpM(j2), tb.lpN(j2), tb.pmM(j2),
-                                tb.pmN(j2), 1 << (J - j2), p.oM, p.oN, S);
-                    emit(S, npath, kbase + (j2 - j1 - 1) * L + l2a, img, p.K, p.oM, p.oN, out, pooled);
+                                tb.pmN(j2), 1 << (J - j2), oM, oN, S);
+                    emit(S, npath, kbase + (j2 - j1 - 1) * L + l2a, img, p.K, oM, oN, out, pooled);
                 }
             }
             // no barrier here: the next batch's fold writes B only, and S is rewritten only after
@@ -1262,6 +1265,21 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
     } else {
         for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2);
     }
+}
+
+
+template <int FM, int FN, int MAXN, int SQ, int HG = 0>
+__global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, LdsLayout lay, int j1, int nimg,
+                                             long long img0, const float2* __restrict__ hexp,
+                                             float* __restrict__ out, int pooled, int j2first) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    if constexpr (SQ && !HG) {
+        if (p.oM == 4 && p.oN == 4 && lay.oms == 4) {
+            k_o2_body<FM, FN, MAXN, SQ, HG, 4>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
+            return;
+        }
+    }
+    k_o2_body<FM, FN, MAXN, SQ, HG, 0>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
 }
 
 }  // namespace wstdev
