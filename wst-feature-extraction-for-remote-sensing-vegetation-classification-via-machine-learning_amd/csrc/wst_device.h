@@ -1073,12 +1073,14 @@ constexpr int o1_min_waves(int cap, int fm, int fn) {
 // ------------------------------------------------------------------------------------------
 // k_o1: one workgroup per (plane, theta1) at fixed j1 -- order 1 + half-spectrum export
 // ------------------------------------------------------------------------------------------
-template <int FM, int FN, int MAXN, int SQ>
-__global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevParams p, LdsLayout lay, int j1, int nimg,
-                                             long long img0, const float2* __restrict__ xhat,
-                                             float2* __restrict__ hexp, float* __restrict__ out,
-                                             int pooled) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// k_o1 body; OC > 0: the output maps are OC x OC (compile-time; the common 4 x 4 of the headline)
+template <int FM, int FN, int MAXN, int SQ, int OC>
+__device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& p,
+                                          const LdsLayout& lay, int j1, int nimg, long long img0,
+                                          const float2* __restrict__ xhat, float2* __restrict__ hexp,
+                                          float* __restrict__ out, int pooled) {
+    const int oM = OC ? OC : p.oM, oN = OC ? OC : p.oN;
+    const int oms = OC ? 4 : lay.oms;
     const int J = p.J, L = p.L;
     const int item = xcd_item(nimg * L);
     const int local = item / L;
@@ -1115,11 +1117,11 @@ __global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevPara
     const int n1idx = j1 * L + l1;
     if (!(dbg & 2)) {
         if constexpr (SQ)
-            lds_lowpass_taps<8, 16>(A, nM1, nN1, ld1, tb.gM(j1), tb.gN(j1), lay.oms, p.oM, p.oN, S);
+            lds_lowpass_taps<8, 16>(A, nM1, nN1, ld1, tb.gM(j1), tb.gN(j1), oms, oM, oN, S);
         else
             lds_lowpass(A, 1, 0, nM1, nN1, ld1, tb.lpM(j1), tb.lpN(j1), tb.pmM(j1), tb.pmN(j1),
-                        1 << (J - j1), p.oM, p.oN, S);
-        emit(S, 1, 1 + n1idx, img, p.K, p.oM, p.oN, out, pooled);
+                        1 << (J - j1), oM, oN, S);
+        emit(S, 1, 1 + n1idx, img, p.K, oM, oN, out, pooled);
     }
     if (!do2) return;
 
@@ -1148,6 +1150,22 @@ __global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevPara
         stnt(d, h0);
         stnt(d + hld, h1);
     }
+}
+
+template <int FM, int FN, int MAXN, int SQ>
+__global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevParams p, LdsLayout lay, int j1, int nimg,
+                                             long long img0, const float2* __restrict__ xhat,
+                                             float2* __restrict__ hexp, float* __restrict__ out,
+                                             int pooled) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // (the 4 x 4 variant measured neutral for the smaller classes: only the 96^2 class carries it)
+    if constexpr (SQ && MAXN == 136) {
+        if (p.oM == 4 && p.oN == 4 && lay.oms == 4) {
+            k_o1_body<FM, FN, MAXN, SQ, 4>(smem, p, lay, j1, nimg, img0, xhat, hexp, out, pooled);
+            return;
+        }
+    }
+    k_o1_body<FM, FN, MAXN, SQ, 0>(smem, p, lay, j1, nimg, img0, xhat, hexp, out, pooled);
 }
 
 // ------------------------------------------------------------------------------------------
