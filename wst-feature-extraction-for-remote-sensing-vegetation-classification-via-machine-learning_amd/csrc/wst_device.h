@@ -1280,6 +1280,16 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             if constexpr ((NN2 << k) == N1C && NN2 >= 1)
                 if (j1 + k < J) level(j1 + k, NN2, NN2);
         });
+    } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {
+        // after a big level the paths start at the first LDS-resident level, which is the
+        // family's single size of this class (> 136 / 2): compile-time sizes from there on
+        constexpr int N2C = unique_level(FM, MAXN);
+        wstfft::static_for<0, 8>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int NN2 = N2C >> k;
+            if constexpr ((NN2 << k) == N2C && NN2 >= 1)
+                if (j2first + k < J) level(j2first + k, NN2, NN2);
+        });
     } else {
         for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2);
     }
@@ -1291,7 +1301,7 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
                                              long long img0, const float2* __restrict__ hexp,
                                              float* __restrict__ out, int pooled, int j2first) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    if constexpr (SQ && !HG) {
+    if constexpr (SQ) {
         if (p.oM == 4 && p.oN == 4 && lay.oms == 4) {
             k_o2_body<FM, FN, MAXN, SQ, HG, 4>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
             return;
