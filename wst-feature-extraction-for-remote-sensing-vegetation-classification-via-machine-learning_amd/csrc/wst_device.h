@@ -104,6 +104,27 @@ __device__ __forceinline__ int reflect_index(int i, int n) {
     return t < n ? t : period - t;
 }
 
+// Sum over aligned groups of G lanes (G a power of two <= 64), every lane of a group receiving the
+// group's sum.  Within a row of 16 lanes the steps are DPP-modified moves (quad_perm [1,0,3,2],
+// [2,3,0,1], row_half_mirror, row_mirror): VALU work instead of ds_bpermute round trips through the
+// LDS crossbar.  A whole group must be active (the callers' loop bounds are multiples of G).
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL,
+                                                                 0xF, 0xF, false));
+}
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+    static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "group size");
+    if constexpr (G >= 2) v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+    if constexpr (G >= 4) v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) v += dpp_mov<0x141>(v);  // row_half_mirror
+    if constexpr (G >= 16) v += dpp_mov<0x140>(v); // row_mirror
+    if constexpr (G >= 32) v += __shfl_xor(v, 16, 64);
+    if constexpr (G >= 64) v += __shfl_xor(v, 32, 64);
+    return v;
+}
+
 __device__ __forceinline__ float block_sum(float v, float* red) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -273,9 +294,7 @@ __device__ __forceinline__ void lds_lowpass_t(float2* U, int nb, int bs, int row
             for (int c = 0; c < OW; ++c) acc[c] = fmaf(x, hq[s * c], acc[c]);
         }
 #pragma unroll
-        for (int off = QC / 2; off >= 1; off >>= 1)
-#pragma unroll
-            for (int c = 0; c < OW; ++c) acc[c] += __shfl_xor(acc[c], off, 64);
+        for (int c = 0; c < OW; ++c) acc[c] = group_sum<QC>(acc[c]);
         if (qc == 0) {
 #pragma unroll
             for (int c = 0; c < OW; ++c)
@@ -295,8 +314,7 @@ __device__ __forceinline__ void lds_lowpass_t(float2* U, int nb, int bs, int row
         float acc = 0.f;
 #pragma unroll 2
         for (int p = pc; p < rows; p += PC) acc = fmaf(h[-(permM ? permM[p] : p)], t[p * ld].y, acc);
-#pragma unroll
-        for (int off = PC / 2; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        acc = group_sum<PC>(acc);
         if (pc == 0) S[o] = acc;
     }
     __syncthreads();
@@ -344,8 +362,7 @@ __device__ __forceinline__ void lds_lowpass_tiled(float2* U, int nb, int bs, int
         for (int r = 0; r < RP; ++r)
 #pragma unroll
             for (int c = 0; c < OW; ++c)
-#pragma unroll
-                for (int off = QC / 2; off >= 1; off >>= 1) acc[r][c] += __shfl_xor(acc[r][c], off, 64);
+                acc[r][c] = group_sum<QC>(acc[r][c]);
         if (qc == 0) {
 #pragma unroll
             for (int r = 0; r < RP; ++r)
@@ -386,8 +403,7 @@ __device__ __forceinline__ void lds_lowpass_tiled(float2* U, int nb, int bs, int
         for (int a = 0; a < AP; ++a)
 #pragma unroll
             for (int c = 0; c < CW; ++c)
-#pragma unroll
-                for (int off = PC / 2; off >= 1; off >>= 1) acc[a][c] += __shfl_xor(acc[a][c], off, 64);
+                acc[a][c] = group_sum<PC>(acc[a][c]);
         if (pc == 0) {
 #pragma unroll
             for (int a = 0; a < AP; ++a)
@@ -450,8 +466,7 @@ __device__ __forceinline__ void lds_lowpass_taps(float2* U, int rows, int cols, 
 #pragma unroll
         for (int c = 0; c < kLpOM; ++c) {
             if (c >= 4 && !w8) break;
-#pragma unroll
-            for (int off = QC / 2; off >= 1; off >>= 1) acc[c] += __shfl_xor(acc[c], off, 64);
+            acc[c] = group_sum<QC>(acc[c]);
         }
         if (qc == 0) {
 #pragma unroll
@@ -485,8 +500,7 @@ __device__ __forceinline__ void lds_lowpass_taps(float2* U, int rows, int cols, 
 #pragma unroll
         for (int a = 0; a < kLpOM; ++a) {
             if (a >= 4 && !w8) break;
-#pragma unroll
-            for (int off = PC / 2; off >= 1; off >>= 1) acc[a] += __shfl_xor(acc[a], off, 64);
+            acc[a] = group_sum<PC>(acc[a]);
         }
         if (pc == 0) {
 #pragma unroll
@@ -602,8 +616,7 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
             });
             acc = fmaf(GN[q * oms + c], wq, acc);
         }
-#pragma unroll
-        for (int off = QC / 2; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        acc = group_sum<QC>(acc);
         if (qc == 0) {
             if (outd) __builtin_nontemporal_store(acc, outd + o);
             else S[o] = acc;

@@ -109,8 +109,7 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
             const int rr = o / p.oN, c = o - (o / p.oN) * p.oN;
             float acc = 0.f;
             for (int q = qc; q < N; q += 8) acc = fmaf(a.gnat[q * a.oms + c], A[rr * ld + q].x, acc);
-#pragma unroll
-            for (int off = 4; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+            acc = wstdev::group_sum<8>(acc);
             if (qc == 0) a.tpart[(static_cast<long long>(arr) * N + r0 + rr) * a.oms + c] = acc;
         }
         float msum = 0.f;   // plane mean from k_big_mean's partials, fixed order (deterministic)
@@ -288,9 +287,7 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
             acc[8] += m;
         }
 #pragma unroll
-        for (int off = PC / 2; off >= 1; off >>= 1)
-#pragma unroll
-            for (int k = 0; k < 9; ++k) acc[k] += __shfl_xor(acc[k], off, 64);
+        for (int k = 0; k < 9; ++k) acc[k] = wstdev::group_sum<PC>(acc[k]);
         if (pc == 0) {
             for (int k = 0; k < p.oM; ++k) a.vpart[(static_cast<long long>(arr) * N + c0 + c) * oms + k] = acc[k];
             a.csum[static_cast<long long>(arr) * N + c0 + c] = acc[8];
