@@ -7,25 +7,35 @@ A "step" = one Scattering2D(J=4, L=8, order 2) pass over one resident batch of 1
 Inputs are synthetic uint8/255 patches (mimicking load_rgb_image, train_and_save_model.py:51-56)
 generated once and resident in HBM before timing.
 
-Multi-GPU (torchrun, one process per GPU): the patches shard across ranks with no data-path
-collective (weak scaling: every rank processes its own 1024-patch batch); value = all patches of
-all ranks / max-over-ranks wall time.  `--gather` additionally times an RCCL all-gather of the
-pooled features (reported separately, never in `value`).
+Multi-GPU (one process per GPU): `bench.py --gpus N` started without WORLD_SIZE launches
+itself as N ranks through torch.distributed.run (the parent never touches the GPU); under an
+external torchrun the world size must equal --gpus.  The patches shard across ranks with no
+data-path collective (weak scaling: every rank processes its own 1024-patch batch); value = all
+patches of all ranks / max-over-ranks wall time.  `--gather` additionally times an RCCL
+all-gather of the pooled features (reported separately, never in `value`).  c3 is the one
+strong-scaling job: 1M patches generated on the devices by global patch index, sharded, pooled,
+and all-gathered inside the timed step.
 
 Extra JSON fields:
   roofline     : dominant kernel (largest HIP-event time of the step; k_o2 at j1=0 on c2)
                  algorithmic FLOP per launch / HIP-event launch time
-                 vs the fp32 peak (SURVEY §8(d) flop convention 5 n^2 log2 n^2 per n x n FFT);
+                 vs the fp32 VALU peak (SURVEY §8(d) flop convention 5 n^2 log2 n^2 per n x n FFT);
+                 also vs FP32_meas (an FMA probe kernel timed in the same run);
                  traffic from committed rocprofv3 PMC passes when they match this library build.
-  cpu_baseline : the float64 oracle (oracle/kymatio_ref.py, a port of kymatio 0.3.0) run the way
-                 the reference runs it (plan rebuilt per patch, 3 serial channel calls + mean/std,
-                 train_and_save_model.py:346-378), single core, bounded sample, rank 0 at N=1.
+  measured     : BW_meas (streaming-copy probe) and FP32_meas (FMA probe), this run, this GPU.
+  cpu_baseline : the float64 oracle (oracle/kymatio_ref.py, a port of kymatio 0.3.0) on the
+                 host cores, rank 0 at every N, before the GPU is touched, bounded sample:
+                 (i) run the way the reference runs it (plan rebuilt per patch, 3 serial channel
+                 calls + mean/std, train_and_save_model.py:346-378), one core = `value`;
+                 (ii) all cores: a fork pool of `workers` processes, cached plan, batched calls.
 """
 import argparse
 import hashlib
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,14 +45,16 @@ sys.path.insert(0, ROOT)
 METRIC = "patches/sec (whole node) + HBM-roofline %, 64x64 RGB WST J=4 L=8 order-2"
 FP32_PEAK_TFLOPS = 157.3      # MI355X FP32 vector == f32 MFMA dense peak (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0         # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+LDS_RESIDENT_MAX = 136        # levels larger than this run HBM-staged (csrc/wst_staged.h)
 
 CONFIGS = {
     "c2": dict(workload="c2: 1024 x 64x64 RGB patches, Scattering2D J=4 L=8 order-2 (per GPU)",
                C=3, M=64, N=64, J=4, L=8, batch=1024),
     "c1": dict(workload="c1: 64x64 RGB patch, J=2 L=8 order-2 (batch as given)",
                C=3, M=64, N=64, J=2, L=8, batch=1024),
-    "c3": dict(workload="c3: 1M synthetic 64x64 RGB patches (generated on device) sharded over the "
-                        "ranks, J=4 L=8 order-2 pooled features + RCCL all-gather (one job per step)",
+    "c3": dict(workload="c3: 1M synthetic 64x64 RGB patches (generated on device by global patch "
+                        "index) sharded over the ranks, J=4 L=8 order-2 pooled features + RCCL "
+                        "all-gather (one job per step)",
                C=3, M=64, N=64, J=4, L=8, batch=1024, total=1_000_000),
     "c4": dict(workload="c4: noise-robustness sweep -- 13 (type, intensity) cases of the reference's "
                         "experiments/ (add_noise.py formulas, device draws) on 1024 64x64 RGB patches, "
@@ -64,6 +76,8 @@ NOISE_SWEEP = [("gaussian", 30), ("gaussian", 50), ("poisson", 40), ("poisson", 
                ("salt_and_pepper", 5), ("salt_and_pepper", 15), ("salt_and_pepper", 25),
                ("speckle", 15), ("speckle", 35), ("speckle", 55),
                ("uniform", 10), ("uniform", 25), ("uniform", 40)]
+
+C3_SEED = 1            # c3 patches: wst_patch_generate(seed=1, global index)
 
 
 def fft_flops(n1, n2):
@@ -96,18 +110,39 @@ def kernel_slots(J, max_order=2):
     return ["k_prep"] + [f"k_o1_j1={j}" for j in range(J)] + [f"k_o2_j1={j}" for j in range(J)]
 
 
+def staged_levels(PM, PN, J):
+    """Leading levels r with max(PM, PN) >> r > 136 run HBM-staged (wst_plan_create's rb)."""
+    rb = 0
+    while rb < J and max(PM, PN) >> rb > LDS_RESIDENT_MAX:
+        rb += 1
+    return rb
+
+
+def family(P):
+    """FFT size family of a padded size: its odd part when compiled (1, 3, 5, 9, 17), else 0."""
+    o = P
+    while o % 2 == 0:
+        o //= 2
+    return o if o in (1, 3, 5, 9, 17) else 0
+
+
 def rocprof_name(slot, PM, PN, J):
-    """Template name rocprofv3 reports for a slot's kernel (size family / size cap)."""
-    def fam(P):
-        o = P
-        while o % 2 == 0:
-            o //= 2
-        return o if o in (1, 3, 5, 9, 17) and P <= 136 else 0
-    fm, fn = fam(PM), fam(PN)
+    """Kernel name (template prefix) rocprofv3 reports for a timing slot.  Slots of HBM-staged
+    levels (j1 < rb, c5's 384^2 / 192^2) run several kernels; they are named by the composite."""
+    fm, fn = family(PM), family(PN)
+    rb = staged_levels(PM, PN, J)
     if slot == "k_prep":
+        if rb:
+            return f"k_big_mean + k_big_rows<{PM}, 0> + k_big_cols<{PM}, 0> + k_big_final"
         return f"k_prep<{fm}, {fn}"
     kind, j1 = slot.split("_j1=")
-    n = max(PM, PN) >> int(j1)
+    j1 = int(j1)
+    if j1 < rb:
+        n = PM >> j1
+        if kind == "k_o1":
+            return f"k_big_rows<{n}, 1> + k_big_cols<{n}, 1> + k_big_final + U1hat k_big_rows/cols<{n}, 0>"
+        return f"staged order-2 k_big_rows/cols + k_big_final + k_o2<{fm}, {fn}, 136, 1, 1"
+    n = max(PM, PN) >> j1
     cap = 12 if n <= 12 else 24 if n <= 24 else 48 if n <= 48 else 136
     return f"{kind}<{fm}, {fn}, {cap}"
 
@@ -151,21 +186,70 @@ def pmc_traffic(sha, kernel):
             if sha not in (d.get("lib_sha"), d.get("src_sha")):
                 continue
             # `kernel` is the template prefix "k_o2<3, 3, 136"; variants append ", SQ, HG>"
-            for name, v in per.items():
-                if name == kernel + ">" or name.startswith(kernel + ","):
+            for kname, v in per.items():
+                if kname == kernel + ">" or kname.startswith(kernel + ","):
                     return v
     return None
 
 
-def cpu_baseline(cfg, budget_s):
-    """Reference-faithful CPU path on the float64 oracle: per patch, Scattering2D rebuilt
-    (train_and_save_model.py:359) and 3 serial channel calls + mean/std (:364-376)."""
-    import numpy as np
+# ------------------------------------------------------------------------------------------
+# CPU baseline (runs on rank 0 before the GPU is touched: the all-cores leg forks)
+# ------------------------------------------------------------------------------------------
+def cpu_workers():
+    """Host cores this process may use: the affinity set, capped by OMP_NUM_THREADS when the
+    environment sets one (the GPU box sets 16 = one GPU's share of the host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _single_thread():
     try:
         from threadpoolctl import threadpool_limits
-        lim = threadpool_limits(1)
+        return threadpool_limits(1)
     except Exception:
-        lim = None
+        return None
+
+
+def _all_cores_worker(cfg, budget_s, seed, conn):
+    """Forked child: cached-plan oracle, batches of 4 patches, until the budget runs out."""
+    import numpy as np
+    _single_thread()
+    from oracle import kymatio_ref as kr
+    sc = kr.Scattering2D(J=cfg["J"], shape=(cfg["M"], cfg["N"]), L=cfg["L"])
+    rng = np.random.default_rng(seed)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        xb = rng.integers(0, 256, (4, cfg["C"], cfg["M"], cfg["N"]), dtype=np.uint8).astype(np.float32) / 255
+        S = sc(xb)
+        np.mean(S, axis=(-2, -1)), np.std(S, axis=(-2, -1))
+        n += 4
+    conn.send((n, time.perf_counter() - t0))
+    conn.close()
+
+
+def cpu_baseline(cfg, budget_s):
+    """(i) Reference-faithful CPU path on the float64 oracle: per patch, Scattering2D rebuilt
+    (train_and_save_model.py:359) and 3 serial channel calls + mean/std (:364-376), one thread.
+    (ii) The same float64 code on every host core this process may use: a fork pool, each worker
+    with a cached plan and batched calls."""
+    import multiprocessing as mp
+
+    import numpy as np
+    lim = _single_thread()
     from oracle import kymatio_ref as kr
     rng = np.random.default_rng(1)
     n, t0 = 0, time.perf_counter()
@@ -177,39 +261,166 @@ def cpu_baseline(cfg, budget_s):
         if el >= budget_s or n >= 256:
             break
     faithful = n / el
-    # cached plan, one batched call (best case for the same float64 code on one core)
-    sc = kr.Scattering2D(J=cfg["J"], shape=(cfg["M"], cfg["N"]), L=cfg["L"])
-    xb = rng.integers(0, 256, (16, cfg["C"], cfg["M"], cfg["N"]), dtype=np.uint8).astype(np.float32) / 255
-    t1 = time.perf_counter()
-    S = sc(xb)
-    np.mean(S, axis=(-2, -1)), np.std(S, axis=(-2, -1))
-    cached = 16 / (time.perf_counter() - t1)
-    if lim is not None:
-        lim.unregister() if hasattr(lim, "unregister") else None
+    if lim is not None and hasattr(lim, "unregister"):
+        lim.unregister()
+    workers = cpu_workers()
+    allc = None
+    if el / n * 4 <= budget_s:         # a worker can finish a few batches inside the budget
+        ctx = mp.get_context("fork")
+        pipes, procs = [], []
+        for w in range(workers):
+            a, b = ctx.Pipe(duplex=False)
+            p = ctx.Process(target=_all_cores_worker, args=(cfg, budget_s, 100 + w, b))
+            p.start()
+            pipes.append(a)
+            procs.append(p)
+        res = [a.recv() for a in pipes]
+        for p in procs:
+            p.join()
+        tot = sum(r[0] for r in res)
+        wall = max(r[1] for r in res)
+        allc = {"value": round(tot / wall, 3), "unit": "patches/s", "cores": workers,
+                "sample": f"{tot} patches over {workers} forked workers in {wall:.1f} s (cached plan, "
+                          f"batches of 4, float64 oracle, one thread each)"}
     return {
         "value": round(faithful, 3), "unit": "patches/s", "cores": 1, "kind": "port",
         "sample": (f"{n} patches of ({cfg['C']},{cfg['M']},{cfg['N']}) in {el:.1f} s: oracle/kymatio_ref.py "
                    f"float64 port of kymatio 0.3.0, plan rebuilt per patch + 3 channel calls + mean/std "
                    f"(train_and_save_model.py:346-378), single thread"),
-        "cached_plan_batched_value": round(cached, 3),
+        "all_cores": allc,
         "host_cpu_count": os.cpu_count(),
         "host_affinity": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None,
+        "cpu_model": _cpu_model(),
     }
+
+
+# ------------------------------------------------------------------------------------------
+# launcher (parent, no GPU) and in-run probes
+# ------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """Re-run this script as n ranks under torch.distributed.run, as a child process (the parent
+    has not touched the GPU and does not exec); returns the launcher's exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def measure_probes(torch, lib, dev, stream):
+    """BW_meas (16-B streaming copy, 1 GiB -> 1 GiB) and FP32_meas (16 FMA chains per lane)."""
+    from wst_amd import _lib
+    nbytes = 1 << 30
+    src = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
+    dst = torch.empty_like(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(2):
+        _lib.check_aux(lib.wst_probe_copy(src.data_ptr(), dst.data_ptr(), nbytes, stream))
+    e0.record()
+    reps = 10
+    for _ in range(reps):
+        _lib.check_aux(lib.wst_probe_copy(src.data_ptr(), dst.data_ptr(), nbytes, stream))
+    e1.record()
+    e1.synchronize()
+    bw = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del src, dst
+    nthreads, iters = 256 * 2048, 4096
+    scratch = torch.empty(nthreads, dtype=torch.float32, device=dev)
+    _lib.check_aux(lib.wst_probe_fma(scratch.data_ptr(), nthreads, iters, stream))
+    e0.record()
+    reps = 5
+    for _ in range(reps):
+        _lib.check_aux(lib.wst_probe_fma(scratch.data_ptr(), nthreads, iters, stream))
+    e1.record()
+    e1.synchronize()
+    tf = 2.0 * 16 * iters * nthreads * reps / (e0.elapsed_time(e1) * 1e-3) / 1e12
+    return {"bw_gbs": round(bw, 1), "fp32_tflops": round(tf, 2),
+            "bw_probe": "16-B/lane non-temporal copy, 1 GiB -> 1 GiB, bytes read + written",
+            "fp32_probe": f"{nthreads} lanes x 16 independent v_fma_f32 chains x {iters} steps"}
+
+
+def launch_check(args, rank, world):
+    """--launch-check: the rank plumbing alone (gloo, no GPU): every rank reports in."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([rank + 1.0])
+    dist.all_reduce(t)
+    ok = world == dist.get_world_size() and t.item() == world * (world + 1) / 2
+    if rank == 0:
+        print(json.dumps({"launch_check": {"world": dist.get_world_size(), "gpus": args.gpus,
+                                           "rank_sum": t.item(), "ok": ok}}), flush=True)
+    dist.destroy_process_group()
+    if not ok:
+        sys.exit(1)
+
+
+def c3_check(cfg, feats, lo, hi, nsample=8):
+    """Recreate `nsample` sampled patches of this rank's shard on the host (oracle/patchgen.py)
+    and compare their pooled features with the float64 oracle (per-feature max-normalised)."""
+    import numpy as np
+    from oracle import kymatio_ref as kr
+    from oracle import patchgen
+    idx = np.random.default_rng(77).choice(cfg["total"], 64 * nsample, replace=False)
+    mine = [int(i) for i in idx if lo <= i < hi][:nsample]
+    if not mine:
+        return 0.0, 0
+    sc = kr.Scattering2D(J=cfg["J"], shape=(cfg["M"], cfg["N"]), L=cfg["L"])
+    ref, got = [], []
+    for i in mine:
+        u8 = patchgen.generate_patches_u8(C3_SEED, i, 1, cfg["C"], cfg["M"], cfg["N"])[0]
+        ref.append(kr.extract_wst_features(u8.astype(np.float32) / 255, J=cfg["J"], L=cfg["L"],
+                                           scattering=sc))
+        got.append(feats[(i - lo) * cfg["C"]:(i - lo + 1) * cfg["C"]].reshape(-1).cpu().numpy())
+    ref, got = np.stack(ref), np.stack(got).astype(np.float64)
+    scale = np.abs(ref).max(axis=0)
+    scale = np.where(scale > 0, scale, 1.0)
+    return float((np.abs(got - ref).max(axis=0) / scale).max()), len(mine)
 
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (ranks); default 1 or WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None, help="patches per GPU (default: config)")
     ap.add_argument("--pooled", action="store_true", help="fused mean/std epilogue output")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL all-gather of features")
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
+    ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU-baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probes", action="store_true", help="skip the BW / FP32 probe kernels")
     ap.add_argument("--profile-iters", type=int, default=3)
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus))          # parent: no GPU call, no exec
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is None:
+        args.gpus = world
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started {world} ranks")
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if args.launch_check:
+        return launch_check(args, rank, world)
+
+    cfg = dict(CONFIGS[args.config])
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfg, args.cpu_budget)      # before any GPU call (the pool forks)
 
     import numpy as np
     import torch
@@ -218,20 +429,16 @@ def main():
     import wst_amd  # noqa: F401
     from wst_amd import _lib
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == args.gpus
 
-    cfg = dict(CONFIGS[args.config])
     B = args.batch or cfg["batch"]
     C, M, N, J, L = cfg["C"], cfg["M"], cfg["N"], cfg["J"], cfg["L"]
     planes = B * C
+    lib = _lib.load()
 
     rng = np.random.default_rng(1 + rank)
     x = torch.from_numpy(rng.integers(0, 256, (B, C, M, N), dtype=np.uint8).astype(np.float32) / 255).to(dev)
@@ -246,10 +453,11 @@ def main():
         plan.forward(x.data_ptr(), planes, out.data_ptr(), args.pooled, ws.data_ptr(), ws_bytes, stream)
 
     units_per_step = B                    # patches one rank processes per step
+    scaling = "weak"
     extra = {}
+    c3_state = None
     if args.config == "c4":
         from wst_amd import noise as wnoise
-        lib = _lib.load()
         x_u8 = torch.from_numpy(rng.integers(0, 256, (B, M, N, C), dtype=np.uint8)).to(dev)
         xin = torch.empty((B, C, M, N), dtype=torch.float32, device=dev)
         feats = torch.empty((len(NOISE_SWEEP), planes, 2 * K), dtype=torch.float32, device=dev)
@@ -271,22 +479,21 @@ def main():
         lo, hi = wdist.shard_range(total, rank, world)
         mine = hi - lo
         feats = torch.empty((mine * C, 2 * K), dtype=torch.float32, device=dev)
-        gen = torch.Generator(device=dev)
-        xb_u8 = torch.empty((B, C, M, N), dtype=torch.uint8, device=dev)
         xb = torch.empty((B, C, M, N), dtype=torch.float32, device=dev)
 
         def step():  # noqa: F811
-            gen.manual_seed(1_000_003 * (rank + 1))
             for b0 in range(0, mine, B):
                 nb = min(B, mine - b0)
-                torch.randint(0, 256, (nb, C, M, N), generator=gen, dtype=torch.uint8, device=dev,
-                              out=xb_u8[:nb])
-                torch.div(xb_u8[:nb], 255.0, out=xb[:nb])
+                # patches lo + b0 .. lo + b0 + nb - 1 of the job, keyed by global index
+                _lib.check_aux(lib.wst_patch_generate(C3_SEED, lo + b0, nb, C, M, N, 1, xb.data_ptr(),
+                                                      stream))
                 plan.forward(xb.data_ptr(), nb * C, feats[b0 * C:].data_ptr(), True, ws.data_ptr(),
                              ws_bytes, stream)
             if world > 1:   # RCCL all-gather of every rank's pooled features (padded shards)
                 wdist.gather_shards(feats.view(mine, C * 2 * K), total)
         units_per_step = mine
+        scaling = "strong"
+        c3_state = (feats, lo, hi)
         extra["c3"] = {"total_patches": total, "patches_this_rank": mine,
                        "gathered_bytes": total * C * 2 * K * 4 if world > 1 else 0}
 
@@ -313,6 +520,17 @@ def main():
     else:
         value = units_per_step * world * args.steps / dt
 
+    if c3_state is not None:        # sampled patches of every shard vs the float64 oracle
+        err, nchk = c3_check(cfg, *c3_state)
+        if world > 1:
+            t = torch.tensor([err, float(nchk)], dtype=torch.float64, device=dev)
+            e2 = t.clone()
+            dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(e2[1:], op=dist.ReduceOp.SUM)
+            err, nchk = t[0].item(), int(e2[1].item())
+        extra["c3"]["oracle_check"] = {"patches": nchk, "max_rel_err": err, "tol": 1e-5,
+                                       "ok": err <= 1e-5}
+
     # per-kernel HIP-event durations on the launch stream (separate, untimed passes)
     slots = kernel_slots(J)
     acc = [0.0] * len(slots)
@@ -327,10 +545,11 @@ def main():
     dom = max(kms, key=kms.get)                     # dominant kernel of the step
     dom_flop = planes * flops[dom]
     achieved = dom_flop / (kms[dom] * 1e-3) / 1e12
+    probes = None if args.no_probes else measure_probes(torch, lib, dev, stream)
     sha = src_sha()
     dname = rocprof_name(dom, plan.PM, plan.PN, J)
     roofline = {
-        "bound": "mfma", "pipe": "fp32 (VALU FFT butterflies; gfx950 f32 MFMA shares the 157.3 TFLOP/s peak)",
+        "bound": "valu", "pipe": "fp32 VALU (LDS FFT butterflies; f32 MFMA only in the wide low-pass)",
         "kernel": f"{dom} ({dname}, ...>)", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
         "traffic": pmc_traffic(sha, dname) or pmc_traffic(lib_sha(), dname),
@@ -341,13 +560,18 @@ def main():
         "all_kernels_tflops": round(planes * sum(flops.values()) / (sum(kms.values()) * 1e-3) / 1e12, 4),
         "src_sha": sha, "lib_sha": lib_sha(),
     }
+    if probes:
+        roofline["peak_measured"] = probes["fp32_tflops"]
+        roofline["frac_of_measured"] = round(achieved / probes["fp32_tflops"], 5)
     patch_flop = C * sum(flops.values())
     patch_bytes = C * M * N * 4 + (C * 2 * K * 4 if args.pooled else C * K * Mo * No * 4)
     rate_per_gpu = value / world
+    bw = probes["bw_gbs"] if probes else HBM_PEAK_GBS
     step_roof = {
         "alg_flop_per_patch": round(patch_flop), "alg_bytes_per_patch": patch_bytes,
         "valu_frac": round(patch_flop * rate_per_gpu / (FP32_PEAK_TFLOPS * 1e12), 5),
         "hbm_roofline_pct": round(100 * patch_bytes * rate_per_gpu / (HBM_PEAK_GBS * 1e9), 5),
+        "hbm_roofline_pct_of_measured": round(100 * patch_bytes * rate_per_gpu / (bw * 1e9), 5),
     }
 
     gather = None
@@ -365,22 +589,20 @@ def main():
         gather = {"what": "pooled features all_gather", "bytes_per_rank": feats.numel() * 4,
                   "ms": round((time.perf_counter() - g0) / 5 * 1e3, 4)}
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, args.cpu_budget)
-
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "patches/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic uint8/255 RGB patches (load_rgb_image distribution), resident in HBM",
             "config": {"workload": cfg["workload"], "patches_per_gpu": units_per_step, "channels": C,
                        "shape": [M, N], "J": J, "L": L, "max_order": 2, "K": K,
                        "output": ("pooled [mean|std]" if (args.pooled or args.config in ("c3", "c4"))
                                   else f"full ({K},{Mo},{No}) fp32"),
-                       "parallelism": f"patch-sharded x{world} (no collective in step)"},
-            "roofline": roofline, "step_roofline": step_roof, "cpu_baseline": cpu,
+                       "parallelism": f"patch-sharded x{world} (no collective in step)"
+                                      if args.config != "c3" else
+                                      f"patch-sharded x{world} + RCCL all-gather of pooled features"},
+            "roofline": roofline, "step_roofline": step_roof, "measured": probes, "cpu_baseline": cpu,
         }
         if gather:
             line["gather"] = gather

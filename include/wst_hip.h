@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define WST_ABI_VERSION 1
+#define WST_ABI_VERSION 2
 
 enum wst_status {
     WST_OK = 0,
@@ -59,6 +59,27 @@ const char* wst_last_error(void);
  */
 int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_plan** out);
 
+/*
+ * Version-dependent constants of kymatio's gabor_2d (recalled from upstream 0.3.0, which is not
+ * in the container): one named plan parameter shared with the oracle's FilterConvention
+ * (oracle/kymatio_ref.py).  wst_plan_create uses wst_default_convention's values:
+ *   norm_pi        = 3.1415  "pi" of the normaliser 2*pi*sigma^2/slant (upstream's literal)
+ *   periodize_half = 2       periodisation copies ex, ey in [-2, 2] (5x5 grid)
+ * tests/test_convention.py measures how far each alternative moves the coefficients relative
+ * to the 1e-5 parity bar.
+ */
+typedef struct wst_filter_convention {
+    double norm_pi;
+    int periodize_half;   /* 0..8 */
+    int reserved;         /* 0 */
+} wst_filter_convention;
+
+int wst_default_convention(wst_filter_convention* out);
+
+/* wst_plan_create with an explicit filter convention (NULL = the default). */
+int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
+                       const wst_filter_convention* conv, wst_plan** out);
+
 /* Release the plan and its device memory. NULL is accepted. */
 int wst_plan_destroy(wst_plan* plan);
 
@@ -84,7 +105,11 @@ int wst_preferred_batch(const wst_plan* plan, int64_t* planes);
  *                   pooled == 1 -> nbatch x 2K: per plane [mean_k (K) | std_k (K)], population
  *                                   std over (Mo, No) -- train_and_save_model.py:371-375 order.
  *   d_workspace / workspace_bytes : caller-owned scratch (see wst_workspace_bytes); NULL/0 lets
- *                   the plan use an internal buffer (allocated on first use; not graph-capturable).
+ *                   the plan use an internal buffer kept per stream (allocated on first use and
+ *                   grown after synchronising that stream; freed with the plan; not
+ *                   graph-capturable).  Calls on different streams never share it; calls that
+ *                   pass their own workspace are re-entrant across streams as long as no two
+ *                   in-flight calls share one workspace.
  *   stream : hipStream_t as void*.
  * Replaces: kymatio scattering2d() over the flattened batch (one call on (B,C,H,W) replaces the
  * reference's B*C serial calls at train_and_save_model.py:364-368 / inference.py:248-254).
@@ -115,6 +140,9 @@ int wst_forward_profiled(const wst_plan* plan, const float* d_in, int64_t nbatch
  */
 int wst_host_filter(int M, int N, int J, int L, int kind, int j, int l, int r, double* out,
                     int64_t len);
+/* wst_host_filter under an explicit filter convention (NULL = the default). */
+int wst_host_filter_ex(int M, int N, int J, int L, int kind, int j, int l, int r,
+                       const wst_filter_convention* conv, double* out, int64_t len);
 
 /*
  * Host emulation of the device line-FFT engine (test hook, no GPU): runs the exact per-unit code
@@ -171,6 +199,28 @@ int wst_noise_generate(int noise_type, double intensity, const uint8_t* d_in, in
  * reproduce numpy / scipy's float32 arithmetic exactly; moments are computed in float64.
  */
 int wst_advanced_stats(const float* d_in, int64_t nplanes, int H, int W, double* d_out, void* stream);
+
+/*
+ * Synthetic patches keyed by (seed, global patch index) -- the c3 data path of SURVEY.md §8(d)
+ * (1M patches generated on the device, each rank its own shard; a patch's bytes never depend on
+ * the rank / chunk split).  Patch p (first_patch <= p < first_patch + npatch), CHW element e:
+ * byte (e & 15) of Philox4x32-10(counter = (e >> 4, 0, p, p >> 32), key = (seed, (seed >> 32) ^
+ * 0x3C6EF372)), little-endian within each 32-bit word.  out_kind 0: uint8 CHW; 1: float32 CHW / 255
+ * (the load_rgb_image distribution of train_and_save_model.py:51-56).
+ */
+int wst_patch_generate(uint64_t seed, int64_t first_patch, int64_t npatch, int C, int H, int W,
+                       int out_kind, void* d_out, void* stream);
+
+/* Batched uint8 HWC (PIL arrays) -> float32 CHW / 255: load_rgb_image's conversion
+ * (train_and_save_model.py:51-56, inference.py:163-168) for nimg images of H x W x C. */
+int wst_u8_to_chw(const uint8_t* d_in, int64_t nimg, int H, int W, int C, float* d_out, void* stream);
+
+/* Measurement probes for bench.py's measured rooflines (SURVEY.md §8(d) BW_meas / FP32_meas;
+ * no kymatio counterpart): a 16-B-per-lane streaming copy of `bytes` (16-byte aligned), and
+ * nthreads (multiple of 256) lanes each running 16 independent FMA chains for `iters` steps
+ * (2 * 16 * iters FLOP per lane). */
+int wst_probe_copy(const void* d_src, void* d_dst, size_t bytes, void* stream);
+int wst_probe_fma(float* d_scratch, int64_t nthreads, int iters, void* stream);
 
 /* Thread-local message of the last failed wst_noise_* / wst_advanced_stats call. */
 const char* wst_aux_last_error(void);

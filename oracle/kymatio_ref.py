@@ -35,6 +35,8 @@ relative difference, far below the 1e-5 parity tolerance).
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
+
 import numpy as np
 import scipy.fft
 
@@ -42,8 +44,33 @@ __all__ = [
     "compute_padding", "gabor_2d", "morlet_2d", "periodize_filter_fft", "filter_bank",
     "reflect_pad", "unpad", "subsample_fourier", "scattering2d", "Scattering2D",
     "num_coefficients", "extract_wst_features", "extract_wst_features_interleaved",
-    "coefficient_index",
+    "coefficient_index", "FilterConvention", "KYMATIO_0_3_0",
 ]
+
+
+# --------------------------------------------------------------------------------------
+# Version-dependent constants of kymatio's filter construction, in ONE place
+# --------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class FilterConvention:
+    """The constants of kymatio's ``gabor_2d`` that are recalled from upstream 0.3.0 rather than
+    read from its source (kymatio is absent: SURVEY.md §8(c)).  The HIP library takes the same
+    struct as its plan parameter (``wst_filter_convention``, include/wst_hip.h; defaults in
+    csrc/filter_bank.h ``kKymatio030``), so oracle and product switch together.
+
+    norm_pi         "pi" of the normaliser 2*pi*sigma^2/slant.  Upstream writes the literal
+                    3.1415 (phi_hat(0) = pi/3.1415).  Every S0 / S1 / S2 scales by
+                    (3.1415/norm_pi)^(1, 2, 3): ~3e-5 / 6e-5 / 9e-5 relative for np.pi.
+    periodize_half  the periodisation grid ex, ey in [-h, h] (5x5 copies for h = 2).
+    gabor_dtype     accumulator of gabor_2d (complex128; complex64 in versions that allocate
+                    ``np.zeros((M, N), np.complex64)``).  Oracle-only switch: the device filters
+                    are float32 either way (tests/test_convention.py measures its effect)."""
+    norm_pi: float = 3.1415
+    periodize_half: int = 2
+    gabor_dtype: type = np.complex128
+
+
+KYMATIO_0_3_0 = FilterConvention()
 
 
 # --------------------------------------------------------------------------------------
@@ -85,31 +112,33 @@ def coefficient_index(J: int, L: int, j1: int, l1: int, j2: int | None = None,
 # --------------------------------------------------------------------------------------
 # A.2 filters
 # --------------------------------------------------------------------------------------
-def gabor_2d(M, N, sigma, theta, xi, slant=1.0, offset=0):
+def gabor_2d(M, N, sigma, theta, xi, slant=1.0, offset=0, conv=KYMATIO_0_3_0):
     """[kymatio 0.3.0] filter_bank.py ``gabor_2d``: periodised (5x5 copies) Gabor in space.
-    ``xx`` runs along axis 0 on the asymmetric grid [ex*M, ex*M + M)."""
-    gab = np.zeros((M, N), np.complex128)
+    ``xx`` runs along axis 0 on the asymmetric grid [ex*M, ex*M + M).  ``conv`` holds the
+    recalled constants (FilterConvention)."""
+    gab = np.zeros((M, N), conv.gabor_dtype)
     R = np.array([[np.cos(theta), -np.sin(theta)], [np.sin(theta), np.cos(theta)]], np.float64)
     R_inv = np.array([[np.cos(theta), np.sin(theta)], [-np.sin(theta), np.cos(theta)]], np.float64)
     D = np.array([[1, 0], [0, slant * slant]])
     curv = np.dot(R, np.dot(D, R_inv)) / (2 * sigma * sigma)
-    for ex in (-2, -1, 0, 1, 2):
-        for ey in (-2, -1, 0, 1, 2):
+    h = conv.periodize_half
+    for ex in range(-h, h + 1):
+        for ey in range(-h, h + 1):
             xx, yy = np.mgrid[offset + ex * M:offset + M + ex * M,
                               offset + ey * N:offset + N + ey * N]
             arg = -(curv[0, 0] * xx * xx + (curv[0, 1] + curv[1, 0]) * xx * yy
                     + curv[1, 1] * yy * yy) \
                 + 1.j * (xx * np.cos(theta) * xi + yy * np.sin(theta) * xi)
             gab += np.exp(arg)
-    norm_factor = 2 * 3.1415 * sigma * sigma / slant   # literal 3.1415, as upstream
+    norm_factor = 2 * conv.norm_pi * sigma * sigma / slant   # literal 3.1415 upstream
     gab /= norm_factor
     return gab
 
 
-def morlet_2d(M, N, sigma, theta, xi, slant=0.5, offset=0):
+def morlet_2d(M, N, sigma, theta, xi, slant=0.5, offset=0, conv=KYMATIO_0_3_0):
     """[kymatio 0.3.0] filter_bank.py ``morlet_2d`` = gabor(xi) - K * gabor(0), zero mean."""
-    wv = gabor_2d(M, N, sigma, theta, xi, slant, offset)
-    wv_modulus = gabor_2d(M, N, sigma, theta, 0, slant, offset)
+    wv = gabor_2d(M, N, sigma, theta, xi, slant, offset, conv)
+    wv_modulus = gabor_2d(M, N, sigma, theta, 0, slant, offset, conv)
     K = np.sum(wv) / np.sum(wv_modulus)
     return wv - K * wv_modulus
 
@@ -155,7 +184,7 @@ def periodize_filter_fft_loops(x, res):
     return crop
 
 
-def filter_bank(M, N, J, L=8):
+def filter_bank(M, N, J, L=8, conv=KYMATIO_0_3_0):
     """[kymatio 0.3.0] filter_bank.py ``filter_bank`` on the PADDED grid (M, N).
 
     psi_{j,l}: sigma=0.8*2^j, theta=(int(L-L/2-1)-l)*pi/L, xi=3pi/(4*2^j), slant=4/L,
@@ -166,12 +195,12 @@ def filter_bank(M, N, J, L=8):
         for theta in range(L):
             psi = {"levels": [], "j": j, "theta": theta}
             psi_signal = morlet_2d(M, N, 0.8 * 2 ** j, (int(L - L / 2 - 1) - theta) * np.pi / L,
-                                   3.0 / 4.0 * np.pi / 2 ** j, 4.0 / L)
+                                   3.0 / 4.0 * np.pi / 2 ** j, 4.0 / L, conv=conv)
             psi_signal_fourier = np.real(scipy.fft.fft2(psi_signal))
             for res in range(min(j + 1, max(J - 1, 1))):
                 psi["levels"].append(periodize_filter_fft(psi_signal_fourier, res))
             filters["psi"].append(psi)
-    phi_signal = gabor_2d(M, N, 0.8 * 2 ** (J - 1), 0, 0)
+    phi_signal = gabor_2d(M, N, 0.8 * 2 ** (J - 1), 0, 0, conv=conv)
     phi_signal_fourier = np.real(scipy.fft.fft2(phi_signal))
     filters["phi"] = {"levels": [], "j": J}
     for res in range(J):
@@ -274,7 +303,7 @@ class Scattering2D:
     """Oracle mirror of kymatio 0.3.0 numpy ``Scattering2D`` (same checks, float64 math)."""
 
     def __init__(self, J, shape, L=8, max_order=2, pre_pad=False, backend=None,
-                 out_type="array"):
+                 out_type="array", convention=KYMATIO_0_3_0):
         self.J, self.L, self.max_order, self.pre_pad = J, L, max_order, pre_pad
         self.out_type = out_type
         self.shape = tuple(shape)
@@ -285,7 +314,7 @@ class Scattering2D:
         self.M_padded, self.N_padded = compute_padding(M, N, J)
         self.pad_size = [(self.M_padded - M) // 2, (self.M_padded - M + 1) // 2,
                          (self.N_padded - N) // 2, (self.N_padded - N + 1) // 2]
-        filters = filter_bank(self.M_padded, self.N_padded, J, L)
+        filters = filter_bank(self.M_padded, self.N_padded, J, L, convention)
         self.phi, self.psi = filters["phi"], filters["psi"]
 
     def _pad(self, x):

@@ -1,4 +1,8 @@
-"""Timing ablation of k_o1 / k_o2 phases (dev tool): per WST_DEBUG_SKIP mask, per-kernel ms."""
+"""Timing ablation of k_o1 / k_o2 phases (dev tool): per WST_DEBUG_SKIP mask, per-kernel ms.
+
+Needs the diagnostic build (the production library ignores WST_DEBUG_SKIP):
+    make -C <pkg>/csrc OUT=../libwst_hip_diag.so OBJ=../build_diag EXTRA=-DWST_DIAG -j16
+and runs it through WST_LIB=libwst_hip_diag.so."""
 import os, subprocess, sys, json
 masks = {"full": 0, "no_o1_fold": 128, "no_o1_ifft": 1, "no_S1": 2, "no_U1_fft": 4, "no_o2_fold": 8,
          "no_o2_ifft": 16, "no_o2_lowpass": 64, "no_order2_paths": 8 | 16 | 64,
@@ -23,7 +27,7 @@ print(json.dumps([a/3 for a in acc]))
 '''
 res = {}
 for name, m in masks.items():
-    env = dict(os.environ, WST_DEBUG_SKIP=str(m))
+    env = dict(os.environ, WST_DEBUG_SKIP=str(m), WST_LIB="libwst_hip_diag.so")
     r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=300)
     line = [l for l in r.stdout.splitlines() if l.startswith("[")]
     res[name] = json.loads(line[-1]) if line else r.stderr[-300:]

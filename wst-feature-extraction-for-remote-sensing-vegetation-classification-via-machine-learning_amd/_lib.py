@@ -16,20 +16,40 @@ LIB_NAME = os.environ.get("WST_LIB", "libwst_hip.so")   # WST_LIB: A/B-test buil
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.path.basename(LIB_NAME))
 
 WST_OK, WST_ERR_INVALID, WST_ERR_UNSUPPORTED, WST_ERR_HIP, WST_ERR_NOMEM = 0, 1, 2, 3, 4
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # every symbol include/wst_hip.h declares
 EXPORTS = (
-    "wst_abi_version", "wst_last_error", "wst_plan_create", "wst_plan_destroy",
+    "wst_abi_version", "wst_last_error", "wst_default_convention", "wst_plan_create",
+    "wst_plan_create_ex", "wst_plan_destroy",
     "wst_output_shape", "wst_padded_shape", "wst_workspace_bytes", "wst_preferred_batch",
     "wst_forward",
-    "wst_forward_profiled", "wst_host_filter", "wst_host_fft_lines",
+    "wst_forward_profiled", "wst_host_filter", "wst_host_filter_ex", "wst_host_fft_lines",
     "wst_salt_pepper_counts", "wst_noise_apply", "wst_noise_generate", "wst_advanced_stats",
+    "wst_patch_generate", "wst_u8_to_chw", "wst_probe_copy", "wst_probe_fma",
     "wst_aux_last_error",
 )
 
 _lib = None
 _lock = threading.Lock()
+
+
+class Convention(ctypes.Structure):
+    """``wst_filter_convention`` (include/wst_hip.h): the recalled kymatio constants, mirrored by
+    ``oracle.kymatio_ref.FilterConvention``.  Defaults = kymatio 0.3.0 (3.1415, 5x5 grid)."""
+    _fields_ = [("norm_pi", ctypes.c_double), ("periodize_half", ctypes.c_int),
+                ("reserved", ctypes.c_int)]
+
+    def __init__(self, norm_pi=3.1415, periodize_half=2):
+        super().__init__(float(norm_pi), int(periodize_half), 0)
+
+
+def _conv_ptr(convention):
+    if convention is None:
+        return None
+    if not isinstance(convention, Convention):   # anything with the two fields (oracle's class)
+        convention = Convention(convention.norm_pi, convention.periodize_half)
+    return ctypes.byref(convention)
 
 
 class WSTError(RuntimeError):
@@ -61,6 +81,15 @@ def load() -> ctypes.CDLL:
         lib.wst_plan_create.restype = c_int
         lib.wst_plan_create.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int,
                                         ctypes.POINTER(c_vp)]
+        conv_p = ctypes.POINTER(Convention)
+        lib.wst_default_convention.restype = c_int
+        lib.wst_default_convention.argtypes = [conv_p]
+        lib.wst_plan_create_ex.restype = c_int
+        lib.wst_plan_create_ex.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, conv_p,
+                                           ctypes.POINTER(c_vp)]
+        lib.wst_host_filter_ex.restype = c_int
+        lib.wst_host_filter_ex.argtypes = [c_int] * 8 + [conv_p, ctypes.POINTER(ctypes.c_double),
+                                                         c_i64]
         lib.wst_plan_destroy.restype = c_int
         lib.wst_plan_destroy.argtypes = [c_vp]
         lib.wst_output_shape.restype = c_int
@@ -81,6 +110,15 @@ def load() -> ctypes.CDLL:
                                            ctypes.c_uint64, c_int, c_vp, c_vp]
         lib.wst_advanced_stats.restype = c_int
         lib.wst_advanced_stats.argtypes = [c_vp, c_i64, c_int, c_int, c_vp, c_vp]
+        lib.wst_patch_generate.restype = c_int
+        lib.wst_patch_generate.argtypes = [ctypes.c_uint64, c_i64, c_i64, c_int, c_int, c_int, c_int,
+                                           c_vp, c_vp]
+        lib.wst_u8_to_chw.restype = c_int
+        lib.wst_u8_to_chw.argtypes = [c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp]
+        lib.wst_probe_copy.restype = c_int
+        lib.wst_probe_copy.argtypes = [c_vp, c_vp, c_sz, c_vp]
+        lib.wst_probe_fma.restype = c_int
+        lib.wst_probe_fma.argtypes = [c_vp, c_i64, c_int, c_vp]
         lib.wst_aux_last_error.restype = ctypes.c_char_p
         lib.wst_aux_last_error.argtypes = []
         lib.wst_preferred_batch.restype = c_int
@@ -121,12 +159,18 @@ def check(code: int) -> None:
         raise WSTError(code, last_error() or f"wst status {code}")
 
 
-def host_filter(M, N, J, L, kind, j, l, r, size) -> np.ndarray:
+def host_filter(M, N, J, L, kind, j, l, r, size, convention=None) -> np.ndarray:
     """Host float64 filter from the library's own construction (no GPU needed)."""
     out = np.zeros(size, np.float64)
-    check(load().wst_host_filter(M, N, J, L, kind, j, l, r,
-                                 out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), size))
+    check(load().wst_host_filter_ex(M, N, J, L, kind, j, l, r, _conv_ptr(convention),
+                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), size))
     return out
+
+
+def default_convention() -> Convention:
+    c = Convention()
+    check(load().wst_default_convention(ctypes.byref(c)))
+    return c
 
 
 def host_fft_lines(data: np.ndarray, n, inverse, nb, bs, nl, ls, es, threads=256, mode=0):
@@ -144,11 +188,11 @@ def host_fft_lines(data: np.ndarray, n, inverse, nb, bs, nl, ls, es, threads=256
 class Plan:
     """Owning handle of a ``wst_plan`` (bound to the device current at creation)."""
 
-    def __init__(self, M, N, J, L, max_order=2, pre_pad=False):
+    def __init__(self, M, N, J, L, max_order=2, pre_pad=False, convention=None):
         lib = load()
         h = ctypes.c_void_p()
-        check(lib.wst_plan_create(int(M), int(N), int(J), int(L), int(max_order),
-                                  1 if pre_pad else 0, ctypes.byref(h)))
+        check(lib.wst_plan_create_ex(int(M), int(N), int(J), int(L), int(max_order),
+                                     1 if pre_pad else 0, _conv_ptr(convention), ctypes.byref(h)))
         self._h = h
         K, Mo, No = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(lib.wst_output_shape(h, ctypes.byref(K), ctypes.byref(Mo), ctypes.byref(No)))

@@ -89,7 +89,8 @@ void fft2(std::vector<cdouble>& a, int rows, int cols, int sign) {
 }
 
 // [kymatio 0.3.0] filter_bank.gabor_2d
-std::vector<cdouble> gabor_2d(int M, int N, double sigma, double theta, double xi, double slant) {
+std::vector<cdouble> gabor_2d(int M, int N, double sigma, double theta, double xi, double slant,
+                              const FilterConvention& conv) {
     std::vector<cdouble> gab(static_cast<size_t>(M) * N, cdouble(0.0, 0.0));
     const double c = std::cos(theta), s = std::sin(theta);
     // curv = R diag(1, slant^2) R^-1 / (2 sigma^2),  R = [[c, -s], [s, c]]
@@ -100,8 +101,9 @@ std::vector<cdouble> gabor_2d(int M, int N, double sigma, double theta, double x
     const double c10 = (s * c * d1 - c * s * d2) * inv;
     const double c11 = (s * s * d1 + c * c * d2) * inv;
     const double cx = c * xi, sy = s * xi;
-    for (int ex = -2; ex <= 2; ++ex) {
-        for (int ey = -2; ey <= 2; ++ey) {
+    const int h = conv.periodize_half;
+    for (int ex = -h; ex <= h; ++ex) {
+        for (int ey = -h; ey <= h; ++ey) {
             for (int i = 0; i < M; ++i) {
                 const double xx = static_cast<double>(ex) * M + i;
                 for (int jj = 0; jj < N; ++jj) {
@@ -113,15 +115,16 @@ std::vector<cdouble> gabor_2d(int M, int N, double sigma, double theta, double x
             }
         }
     }
-    const double norm = 2.0 * 3.1415 * sigma * sigma / slant;  // literal 3.1415, as upstream
+    const double norm = 2.0 * conv.norm_pi * sigma * sigma / slant;  // literal 3.1415 upstream
     for (auto& v : gab) v /= norm;
     return gab;
 }
 
 // [kymatio 0.3.0] filter_bank.morlet_2d
-std::vector<cdouble> morlet_2d(int M, int N, double sigma, double theta, double xi, double slant) {
-    std::vector<cdouble> wv = gabor_2d(M, N, sigma, theta, xi, slant);
-    std::vector<cdouble> wm = gabor_2d(M, N, sigma, theta, 0.0, slant);
+std::vector<cdouble> morlet_2d(int M, int N, double sigma, double theta, double xi, double slant,
+                               const FilterConvention& conv) {
+    std::vector<cdouble> wv = gabor_2d(M, N, sigma, theta, xi, slant, conv);
+    std::vector<cdouble> wm = gabor_2d(M, N, sigma, theta, 0.0, slant, conv);
     cdouble sw(0.0, 0.0), sm(0.0, 0.0);
     for (size_t i = 0; i < wv.size(); ++i) { sw += wv[i]; sm += wm[i]; }
     const cdouble K = sw / sm;
@@ -170,11 +173,11 @@ std::vector<double> periodize_1d(const std::vector<double>& x, int n, int res) {
     return crop;
 }
 
-// 1-D periodised Gaussian g(x) = sum_{e=-2..2} exp(-(x + e n)^2 / (2 sigma^2)) on [0, n): the
+// 1-D periodised Gaussian g(x) = sum_{e=-h..h} exp(-(x + e n)^2 / (2 sigma^2)) on [0, n): the
 // separable factor of gabor_2d(sigma, theta=0, xi=0, slant=1) (phi).
-static std::vector<double> gauss_1d(int n, double sigma) {
+static std::vector<double> gauss_1d(int n, double sigma, int h) {
     std::vector<double> g(static_cast<size_t>(n), 0.0);
-    for (int e = -2; e <= 2; ++e)
+    for (int e = -h; e <= h; ++e)
         for (int i = 0; i < n; ++i) {
             const double x = static_cast<double>(e) * n + i;
             g[i] += std::exp(-x * x / (2.0 * sigma * sigma));
@@ -182,9 +185,10 @@ static std::vector<double> gauss_1d(int n, double sigma) {
     return g;
 }
 
-FilterBank build_filter_bank(const Geometry& g) {
+FilterBank build_filter_bank(const Geometry& g, const FilterConvention& conv) {
     FilterBank fb;
     fb.g = g;
+    fb.conv = conv;
     const int PM = g.PM, PN = g.PN, J = g.J, L = g.L;
     // [kymatio 0.3.0] filter_bank: psi_{j, theta}
     fb.psi.resize(static_cast<size_t>(J) * L);
@@ -194,7 +198,7 @@ FilterBank build_filter_bank(const Geometry& g) {
             const double theta = (static_cast<int>(L - L / 2.0 - 1) - t) * kPi / L;
             const double xi = 3.0 / 4.0 * kPi / std::ldexp(1.0, j);
             const double slant = 4.0 / L;
-            std::vector<cdouble> sig = morlet_2d(PM, PN, sigma, theta, xi, slant);
+            std::vector<cdouble> sig = morlet_2d(PM, PN, sigma, theta, xi, slant, conv);
             fft2(sig, PM, PN, -1);
             std::vector<double> re(sig.size());
             for (size_t i = 0; i < sig.size(); ++i) re[i] = sig[i].real();
@@ -202,15 +206,15 @@ FilterBank build_filter_bank(const Geometry& g) {
             for (int r = 0; r < psi_levels(j, J); ++r) levels.push_back(periodize_filter_fft(re, PM, PN, r));
         }
     }
-    // phi = gabor_2d(sigma=0.8*2^(J-1), theta=0, xi=0, slant=1) = gM(x) gN(y) / (2*3.1415*sigma^2)
+    // phi = gabor_2d(sigma=0.8*2^(J-1), theta=0, xi=0, slant=1) = gM(x) gN(y) / (2*norm_pi*sigma^2)
     // phi_hat = Re(fft2(phi)) = Re(GM) Re(GN) / norm - Im(GM) Im(GN) / norm; the second term is
     // checked to be negligible (gM symmetric), so every masked-crop level is the outer product
     // of two 1-D crops.  J == 0 has no phi level used by the cascade except level 0 semantics
     // of S0 (kymatio builds range(J) levels; S0 then uses level 0 -> we need J >= 1 levels).
     const double sigma_phi = 0.8 * std::ldexp(1.0, J - 1);
-    const double norm = 2.0 * 3.1415 * sigma_phi * sigma_phi;
+    const double norm = 2.0 * conv.norm_pi * sigma_phi * sigma_phi;
     auto spectrum_1d = [&](int n, std::vector<double>& re_out) {
-        std::vector<double> gs = gauss_1d(n, sigma_phi);
+        std::vector<double> gs = gauss_1d(n, sigma_phi, conv.periodize_half);
         std::vector<cdouble> G(gs.begin(), gs.end());
         dft_inplace(G.data(), n, 1, -1);
         double mre = 0.0, mim = 0.0;

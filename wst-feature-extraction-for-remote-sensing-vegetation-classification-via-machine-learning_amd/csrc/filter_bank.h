@@ -14,6 +14,16 @@ namespace wst {
 
 using cdouble = std::complex<double>;
 
+// Version-dependent constants of kymatio's gabor_2d, recalled from upstream 0.3.0 (kymatio is
+// not in the container: SURVEY.md §8(c)).  One struct, mirrored by the oracle's
+// FilterConvention (oracle/kymatio_ref.py) and exposed as the plan parameter
+// wst_filter_convention (include/wst_hip.h), so the oracle and the product switch together.
+struct FilterConvention {
+    double norm_pi = 3.1415;   // "pi" of gabor_2d's normaliser 2*pi*sigma^2/slant (literal 3.1415)
+    int periodize_half = 2;    // periodisation copies ex, ey in [-h, h] (5x5 grid)
+};
+constexpr FilterConvention kKymatio030{3.1415, 2};
+
 struct Geometry {
     int M = 0, N = 0;     // input plane
     int J = 0, L = 0;
@@ -35,8 +45,10 @@ void dft_inplace(cdouble* x, int n, int stride, int sign);
 void fft2(std::vector<cdouble>& a, int rows, int cols, int sign);
 
 // gabor_2d / morlet_2d on an (M, N) grid, row-major.
-std::vector<cdouble> gabor_2d(int M, int N, double sigma, double theta, double xi, double slant);
-std::vector<cdouble> morlet_2d(int M, int N, double sigma, double theta, double xi, double slant);
+std::vector<cdouble> gabor_2d(int M, int N, double sigma, double theta, double xi, double slant,
+                              const FilterConvention& conv = kKymatio030);
+std::vector<cdouble> morlet_2d(int M, int N, double sigma, double theta, double xi, double slant,
+                               const FilterConvention& conv = kKymatio030);
 
 // Masked crop of a real (M, N) spectrum to level `res` -> (M>>res, N>>res).
 std::vector<double> periodize_filter_fft(const std::vector<double>& x, int M, int N, int res);
@@ -51,6 +63,7 @@ inline int psi_levels(int j, int J) {
 
 struct FilterBank {
     Geometry g;
+    FilterConvention conv;
     // psi[(j*L + l)][r] : (PM>>r) x (PN>>r) real Fourier filter, row-major
     std::vector<std::vector<std::vector<double>>> psi;
     // 1-D factors of phi's Fourier levels: phi_hat^r(k, l) = aM[r][k] * aN[r][l]
@@ -61,6 +74,6 @@ struct FilterBank {
 
 // Build the full bank (float64).  Throws std::runtime_error on internal inconsistency (e.g. a
 // phi spectrum that is not separable to 1e-12, which would invalidate the separable low-pass).
-FilterBank build_filter_bank(const Geometry& g);
+FilterBank build_filter_bank(const Geometry& g, const FilterConvention& conv = kKymatio030);
 
 }  // namespace wst

@@ -6,6 +6,9 @@
 //   F4  advanced_stats -- src/training/train_and_save_model.py:58-112, one workgroup per plane:
 //       moments, exact float32 numpy percentiles (bitonic sort in LDS), scipy sobel / laplace
 //       with their exact float32 rounding order, edge density.
+//   c3  synthetic patches keyed by (seed, global patch index): k_patch_generate
+//   F3  batched uint8 HWC -> float32 CHW / 255 ingest: k_u8_to_chw
+//   probes for bench.py's measured rooflines: k_probe_copy (HBM), k_probe_fma (FP32 VALU)
 // Inputs are the reference's formats: uint8 HWC images (PIL arrays) in, uint8 HWC (what
 // add_noise.py saves) or float32 CHW / 255 (load_rgb_image, train_and_save_model.py:51-56) out.
 #include <hip/hip_runtime.h>
@@ -377,6 +380,85 @@ __global__ void __launch_bounds__(kStatThreads) k_advanced_stats(const float* __
     }
 }
 
+// ---- synthetic patches keyed by (seed, global patch index) ----
+// Element e of patch p (CHW order, e < C*H*W) is byte (e & 15) of the 16-byte Philox4x32-10
+// block counter (e >> 4, 0, p, p >> 32) under key (seed, seed >> 32 ^ 0x3C6EF372): a patch's
+// values never depend on how the patches are split across ranks or chunks.  out_kind 0: uint8
+// CHW; 1: float32 CHW / 255 (the load_rgb_image distribution, train_and_save_model.py:51-56).
+// One thread per 16-byte block.
+__global__ void k_patch_generate(unsigned long long seed, long long first, long long npatch,
+                                 long long per, int out_kind, void* out) {
+    const long long nblk = (per + 15) >> 4;
+    const uint32_t k0 = static_cast<uint32_t>(seed), k1 = static_cast<uint32_t>(seed >> 32) ^ 0x3C6EF372u;
+    for (long long t = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; t < npatch * nblk;
+         t += static_cast<long long>(gridDim.x) * blockDim.x) {
+        const long long lp = t / nblk, q = t - lp * nblk;
+        const unsigned long long p = static_cast<unsigned long long>(first + lp);
+        const U4 r = philox(U4{static_cast<uint32_t>(q), static_cast<uint32_t>(q >> 32),
+                               static_cast<uint32_t>(p), static_cast<uint32_t>(p >> 32)}, k0, k1);
+        const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+        const long long e0 = q << 4;
+        const long long n = per - e0 < 16 ? per - e0 : 16;
+        if (out_kind == 0) {
+            uint8_t* o = static_cast<uint8_t*>(out) + lp * per + e0;
+            for (int k = 0; k < n; ++k) o[k] = static_cast<uint8_t>(w[k >> 2] >> (8 * (k & 3)));
+        } else {
+            float* o = static_cast<float*>(out) + lp * per + e0;
+            for (int k = 0; k < n; ++k)
+                o[k] = static_cast<float>(static_cast<uint8_t>(w[k >> 2] >> (8 * (k & 3)))) / 255.0f;
+        }
+    }
+}
+
+// ---- uint8 HWC -> float32 CHW / 255 (load_rgb_image's ingest, train_and_save_model.py:51-56) ----
+// One thread per 4 consecutive pixels of a row-major image: 4*C bytes in, four floats to each
+// of the C planes (float4 stores when the row of 4 is aligned and complete).
+__global__ void k_u8_to_chw(const uint8_t* __restrict__ in, long long nimg, int HW, int C,
+                            float* __restrict__ out) {
+    const long long q4 = (HW + 3) >> 2;
+    for (long long t = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; t < nimg * q4;
+         t += static_cast<long long>(gridDim.x) * blockDim.x) {
+        const long long img = t / q4;
+        const int p0 = static_cast<int>(t - img * q4) << 2;
+        const int np_ = HW - p0 < 4 ? HW - p0 : 4;
+        const uint8_t* src = in + (img * HW + p0) * C;
+        float* dst = out + img * C * static_cast<long long>(HW) + p0;
+        for (int ch = 0; ch < C; ++ch) {
+            float v[4];
+            for (int k = 0; k < 4; ++k) v[k] = k < np_ ? static_cast<float>(src[k * C + ch]) / 255.0f : 0.f;
+            float* d = dst + static_cast<long long>(ch) * HW;
+            if (np_ == 4 && (reinterpret_cast<uintptr_t>(d) & 15) == 0) {
+                *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+                for (int k = 0; k < np_; ++k) d[k] = v[k];
+            }
+        }
+    }
+}
+
+// ---- measurement probes (bench.py: BW_meas, FP32_meas of SURVEY.md §8(d)) ----
+// Streaming copy, 16 B per lane per access, grid-stride.
+typedef float v4f __attribute__((ext_vector_type(4)));
+__global__ void k_probe_copy(const v4f* __restrict__ src, v4f* __restrict__ dst, long long n) {
+    for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n;
+         i += static_cast<long long>(gridDim.x) * blockDim.x)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+// 16 independent FMA chains per lane; a, b are runtime values so nothing folds.
+__global__ void __launch_bounds__(256) k_probe_fma(float* out, int iters, float a, float b) {
+    float acc[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[k] = static_cast<float>(threadIdx.x + k);
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc[k] = fmaf(acc[k], a, b);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += acc[k];
+    if (s == 1234.5f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;   // never true: keeps the work
+}
+
 thread_local std::string g_aux_error;
 
 int aux_fail(int code, const char* msg) {
@@ -463,6 +545,57 @@ int wst_noise_generate(int noise_type, double intensity, const uint8_t* d_in, in
                                static_cast<long long>(np_), H, W, C, static_cast<unsigned long long>(seed), 1,
                                0, out_kind, d_out);
     }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return aux_fail(WST_ERR_HIP, hipGetErrorString(e));
+    return WST_OK;
+}
+
+int wst_patch_generate(uint64_t seed, int64_t first_patch, int64_t npatch, int C, int H, int W,
+                       int out_kind, void* d_out, void* stream) {
+    if (first_patch < 0 || npatch < 0 || C < 1 || H < 1 || W < 1 || out_kind < 0 || out_kind > 1)
+        return aux_fail(WST_ERR_INVALID, "bad arguments");
+    if (npatch == 0) return WST_OK;
+    if (!d_out) return aux_fail(WST_ERR_INVALID, "output pointer is NULL");
+    const long long per = static_cast<long long>(C) * H * W;
+    hipLaunchKernelGGL(k_patch_generate, grid_for(npatch * ((per + 15) >> 4), 256), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), static_cast<unsigned long long>(seed),
+                       static_cast<long long>(first_patch), static_cast<long long>(npatch), per, out_kind,
+                       d_out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return aux_fail(WST_ERR_HIP, hipGetErrorString(e));
+    return WST_OK;
+}
+
+int wst_u8_to_chw(const uint8_t* d_in, int64_t nimg, int H, int W, int C, float* d_out, void* stream) {
+    if (nimg < 0 || H < 1 || W < 1 || C < 1) return aux_fail(WST_ERR_INVALID, "bad arguments");
+    if (nimg == 0) return WST_OK;
+    if (!d_in || !d_out) return aux_fail(WST_ERR_INVALID, "input/output pointer is NULL");
+    const int HW = H * W;
+    hipLaunchKernelGGL(k_u8_to_chw, grid_for(nimg * ((HW + 3) / 4), 256), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), d_in, static_cast<long long>(nimg), HW, C,
+                       d_out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return aux_fail(WST_ERR_HIP, hipGetErrorString(e));
+    return WST_OK;
+}
+
+int wst_probe_copy(const void* d_src, void* d_dst, size_t bytes, void* stream) {
+    if (!d_src || !d_dst || (bytes & 15) || (reinterpret_cast<uintptr_t>(d_src) & 15) ||
+        (reinterpret_cast<uintptr_t>(d_dst) & 15))
+        return aux_fail(WST_ERR_INVALID, "copy probe needs 16-byte aligned buffers and size");
+    const long long n = static_cast<long long>(bytes / 16);
+    hipLaunchKernelGGL(k_probe_copy, dim3(256 * 32), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       static_cast<const v4f*>(d_src), static_cast<v4f*>(d_dst), n);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return aux_fail(WST_ERR_HIP, hipGetErrorString(e));
+    return WST_OK;
+}
+
+int wst_probe_fma(float* d_scratch, int64_t nthreads, int iters, void* stream) {
+    if (!d_scratch || nthreads < 256 || (nthreads % 256) || iters < 1)
+        return aux_fail(WST_ERR_INVALID, "fma probe: nthreads a positive multiple of 256, iters >= 1");
+    hipLaunchKernelGGL(k_probe_fma, dim3(static_cast<unsigned>(nthreads / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), d_scratch, iters, 0.999f, 1e-3f);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return aux_fail(WST_ERR_HIP, hipGetErrorString(e));
     return WST_OK;

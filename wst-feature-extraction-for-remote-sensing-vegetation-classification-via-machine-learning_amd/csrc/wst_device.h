@@ -46,6 +46,14 @@ __device__ unsigned long long wst_stamps[kStampBlocks * kStampSlots];
 #define WST_LP_TILED 1  // register-tiled separable low-pass for outputs wider than 8 (lds_lowpass)
 #endif
 
+// Phase-skipping ablation mask (DevParams::dbg_skip): compiled in only for diagnostic builds
+// (-DWST_DIAG); production kernels see a constant 0 and carry no skip branches.
+#ifdef WST_DIAG
+#define WST_DBG_MASK(p) ((p).dbg_skip)
+#else
+#define WST_DBG_MASK(p) 0
+#endif
+
 namespace wstdev {
 
 constexpr int kMaxLds = 160 * 1024;
@@ -55,7 +63,7 @@ constexpr int kMaxO = 8;  // outputs per thread per generic-DFT chunk
 struct DevParams {
     int M, N, PM, PN, J, L, max_order, pre_pad, K;
     int mM, mN, oM, oN, padTop, padLeft;
-    int dbg_skip;                 // timing-ablation mask (env WST_DEBUG_SKIP; 0 in production)
+    int dbg_skip;                 // timing-ablation mask (env WST_DEBUG_SKIP, WST_DIAG builds only)
     const float* psi;             // concatenated psi Fourier levels (fp32)
     const long long* psi_off;     // [(j*L + l)*J + r]
     const float* lp;              // spatial low-pass taps per level, each stored twice
@@ -1108,7 +1116,7 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     float* S = reinterpret_cast<float*>(smem + lay.off_s);
     float* red = reinterpret_cast<float*>(smem + lay.off_red);
     const Tables tb = load_tables(p, lay, smem);
-    const int dbg = p.dbg_skip;
+    const int dbg = WST_DBG_MASK(p);
 
     // 1. fold_{2^j1}(Xhat * psi0_{j1,l1}) straight from HBM/L2
     const float* psi0 = p.psi + p.psi_off[(j1 * L + l1) * J + 0];
@@ -1214,7 +1222,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     float2* B = reinterpret_cast<float2*>(smem + lay.off_b);
     float* S = reinterpret_cast<float*>(smem + lay.off_s);
     const Tables tb = load_tables(p, lay, smem);
-    const int dbg = p.dbg_skip;
+    const int dbg = WST_DBG_MASK(p);
     wstfft::EpiIdentity id;
     [[maybe_unused]] int sctr = 0;
     [[maybe_unused]] const bool stamp_on = (j1 == 0);

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -90,9 +91,21 @@ int fill_cu(int threads, size_t lds) {
     return threads;
 }
 
-// "t0,t1,..." tuning override of per-j1 thread counts
+// Tuning / ablation knobs read from the environment exist only in diagnostic builds
+// (make EXTRA=-DWST_DIAG): a production library never changes its algorithm, launch shape or
+// results because of an inherited variable.
+const char* diag_env(const char* name) {
+#ifdef WST_DIAG
+    return std::getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
+// "t0,t1,..." tuning override of per-j1 thread counts (diagnostic builds)
 void threads_override(const char* env, std::vector<int>& v) {
-    const char* s = std::getenv(env);
+    const char* s = diag_env(env);
     if (!s) return;
     int j = 0;
     for (const char* c = s; *c && j < static_cast<int>(v.size()); ++j) {
@@ -158,10 +171,16 @@ struct wst_plan {
     size_t ws_xhat = 0;
     std::vector<size_t> ws_h_off;   // byte offset of level j1's half spectra (per plane units)
     size_t ws_plane = 0;
-    // internal workspace (used when the caller passes none)
+    // internal workspaces (used when the caller passes none), one per stream: calls on one
+    // stream are ordered by the stream, calls on different streams never share scratch.  ws_mu
+    // is held while a call enqueues on its buffer, so a buffer is only grown (stream-synchronised,
+    // then freed) when no other host thread is between fetching it and launching on it.
+    struct StreamWs {
+        void* ptr = nullptr;
+        size_t bytes = 0;
+    };
     mutable std::mutex ws_mu;
-    mutable void* ws = nullptr;
-    mutable size_t ws_bytes = 0;
+    mutable std::map<hipStream_t, StreamWs> ws_by_stream;
 };
 
 namespace {
@@ -185,7 +204,8 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_lpt);
     (void)hipFree(p->d_lpt_off);
     (void)hipFree(p->d_lpn);
-    if (p->ws) (void)hipFree(p->ws);
+    for (auto& kv : p->ws_by_stream)
+        if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     delete p;
 }
 
@@ -301,6 +321,20 @@ int cyclic_window(const std::vector<char>& hit) {
     return start | (len << 8);
 }
 
+// C-ABI convention -> host struct (NULL = kymatio 0.3.0 as recalled); false on a bad value.
+bool to_convention(const wst_filter_convention* c, wst::FilterConvention& out) {
+    out = wst::kKymatio030;
+    if (!c) return true;
+    if (!(c->norm_pi > 0.0) || c->periodize_half < 0 || c->periodize_half > 8 || c->reserved != 0) {
+        fail(WST_ERR_INVALID, "bad wst_filter_convention (norm_pi > 0, 0 <= periodize_half <= 8, "
+                              "reserved == 0)");
+        return false;
+    }
+    out.norm_pi = c->norm_pi;
+    out.periodize_half = c->periodize_half;
+    return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -309,16 +343,31 @@ int wst_abi_version(void) { return WST_ABI_VERSION; }
 
 const char* wst_last_error(void) { return g_last_error.c_str(); }
 
+int wst_default_convention(wst_filter_convention* out) {
+    if (!out) return fail(WST_ERR_INVALID, "out is NULL");
+    out->norm_pi = wst::kKymatio030.norm_pi;
+    out->periodize_half = wst::kKymatio030.periodize_half;
+    out->reserved = 0;
+    return WST_OK;
+}
+
 int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_plan** out) {
+    return wst_plan_create_ex(M, N, J, L, max_order, pre_pad, nullptr, out);
+}
+
+int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
+                       const wst_filter_convention* conv_in, wst_plan** out) {
     if (!out) return fail(WST_ERR_INVALID, "out is NULL");
     *out = nullptr;
     if (J < 1) return fail(WST_ERR_INVALID, "J must be >= 1 (kymatio needs phi level 0)");
+    wst::FilterConvention conv;
+    if (!to_convention(conv_in, conv)) return WST_ERR_INVALID;
     wst::Geometry g;
     std::string err;
     if (!wst::make_geometry(M, N, J, L, max_order, g, err)) return fail(WST_ERR_INVALID, err);
     wst::FilterBank fb;
     try {
-        fb = wst::build_filter_bank(g);
+        fb = wst::build_filter_bank(g, conv);
     } catch (const std::exception& e) {
         return fail(WST_ERR_UNSUPPORTED, e.what());
     }
@@ -419,7 +468,7 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
                                     csig[kc] = 1;
                                 }
                     }
-                    if (const char* e = std::getenv("WST_BOX"))   // 0: dense fold (A/B timing)
+                    if (const char* e = diag_env("WST_BOX"))   // 0: dense fold (A/B timing)
                         if (std::atoi(e) == 0) std::fill(rsig.begin(), rsig.end(), 1), std::fill(csig.begin(), csig.end(), 1);
                     std::vector<char> hit(sa);
                     for (int u = 0; u < nM2; ++u) {
@@ -448,7 +497,7 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
                         rsig[kr] = 1;
                         csig[kc] = 1;
                     }
-            if (const char* e = std::getenv("WST_BOX"))
+            if (const char* e = diag_env("WST_BOX"))
                 if (std::atoi(e) == 0) continue;
             box1_off[static_cast<size_t>(j) * L + l] = static_cast<int>(box.size());
             std::vector<char> hit(sa);
@@ -549,7 +598,8 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     dp.mM = g.mM; dp.mN = g.mN; dp.oM = g.oM; dp.oN = g.oN;
     dp.padTop = g.padTop; dp.padLeft = g.padLeft;
     {
-        const char* dbg = std::getenv("WST_DEBUG_SKIP");
+        // phase-skipping timing ablation: diagnostic builds only (the results are wrong by design)
+        const char* dbg = diag_env("WST_DEBUG_SKIP");
         dp.dbg_skip = dbg ? std::atoi(dbg) : 0;
     }
     dp.psi = plan->d_psi; dp.psi_off = plan->d_psi_off;
@@ -562,7 +612,7 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
     // the order-1 box-sparse fold pays off from s = 8 on (measured on MI355X at c2); order 2
     // uses it for every s >= 4
     dp.box1_min_s = 8;
-    if (const char* e = std::getenv("WST_BOX1_MIN_S")) dp.box1_min_s = std::atoi(e);
+    if (const char* e = diag_env("WST_BOX1_MIN_S")) dp.box1_min_s = std::atoi(e);
     dp.lpt = plan->d_lpt; dp.lpt_off = plan->d_lpt_off;
     // square variant (bounded FFT sizes + fused order-2 low-pass): square plane of a compiled
     // family, oM <= kLpOM and every order-2 level's column units hold ceil(oM / 2) slots
@@ -570,7 +620,7 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
                 g.oM <= wstdev::kLpOM) ? 1 : 0;
     for (int j2 = 1; j2 < J; ++j2)
         if (rows_per_unit(g.PM >> j2) < (g.oM + 1) / 2) plan->sq = 0;
-    if (const char* e = std::getenv("WST_SQ")) plan->sq = plan->sq && std::atoi(e) != 0;
+    if (const char* e = diag_env("WST_SQ")) plan->sq = plan->sq && std::atoi(e) != 0;
 
     // --- LDS layouts ---
     const size_t omn = static_cast<size_t>(g.oM) * g.oN;
@@ -984,22 +1034,25 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
     const size_t plane_ws = plan->ws_plane;
     void* ws = d_workspace;
     size_t wsb = workspace_bytes;
+    std::unique_lock<std::mutex> ws_lock;   // held through the enqueue on an internal buffer
     if (!ws) {
-        // internal workspace: up to max_chunk planes per chunk
+        // internal workspace of this stream: up to max_chunk planes per chunk
         const int64_t want = std::min<int64_t>(nbatch, plan->max_chunk);
-        std::lock_guard<std::mutex> lk(plan->ws_mu);
-        if (plan->ws_bytes < want * plane_ws) {
-            if (plan->ws) {
+        ws_lock = std::unique_lock<std::mutex>(plan->ws_mu);
+        wst_plan::StreamWs& sw = plan->ws_by_stream[stream];
+        if (sw.bytes < static_cast<size_t>(want) * plane_ws) {
+            if (sw.ptr) {
+                // only this stream's calls use the buffer: once it drains, the buffer is idle
                 WST_HIP_CHECK(hipStreamSynchronize(stream));
-                (void)hipFree(plan->ws);
-                plan->ws = nullptr;
-                plan->ws_bytes = 0;
+                (void)hipFree(sw.ptr);
+                sw.ptr = nullptr;
+                sw.bytes = 0;
             }
-            WST_HIP_CHECK(hipMalloc(&plan->ws, want * plane_ws));
-            plan->ws_bytes = want * plane_ws;
+            WST_HIP_CHECK(hipMalloc(&sw.ptr, static_cast<size_t>(want) * plane_ws));
+            sw.bytes = static_cast<size_t>(want) * plane_ws;
         }
-        ws = plan->ws;
-        wsb = plan->ws_bytes;
+        ws = sw.ptr;
+        wsb = sw.bytes;
     }
     const int64_t chunk = std::min<int64_t>(static_cast<int64_t>(wsb / plane_ws), plan->max_chunk);
     if (chunk < 1) return fail(WST_ERR_INVALID, "workspace smaller than one plane's share");
@@ -1056,7 +1109,14 @@ int wst_forward_profiled(const wst_plan* plan, const float* d_in, int64_t nbatch
 
 int wst_host_filter(int M, int N, int J, int L, int kind, int j, int l, int r, double* out,
                     int64_t len) {
+    return wst_host_filter_ex(M, N, J, L, kind, j, l, r, nullptr, out, len);
+}
+
+int wst_host_filter_ex(int M, int N, int J, int L, int kind, int j, int l, int r,
+                       const wst_filter_convention* conv_in, double* out, int64_t len) {
     if (!out) return fail(WST_ERR_INVALID, "out is NULL");
+    wst::FilterConvention conv;
+    if (!to_convention(conv_in, conv)) return WST_ERR_INVALID;
     if (J < 1) return fail(WST_ERR_INVALID, "J must be >= 1");
     wst::Geometry g;
     std::string err;
@@ -1064,8 +1124,9 @@ int wst_host_filter(int M, int N, int J, int L, int kind, int j, int l, int r, d
     try {
         // cache the last bank: the test-suite inspects every filter of one geometry in turn
         static thread_local std::unique_ptr<wst::FilterBank> cached;
-        if (!cached || cached->g.M != M || cached->g.N != N || cached->g.J != J || cached->g.L != L)
-            cached.reset(new wst::FilterBank(wst::build_filter_bank(g)));
+        if (!cached || cached->g.M != M || cached->g.N != N || cached->g.J != J || cached->g.L != L ||
+            cached->conv.norm_pi != conv.norm_pi || cached->conv.periodize_half != conv.periodize_half)
+            cached.reset(new wst::FilterBank(wst::build_filter_bank(g, conv)));
         const wst::FilterBank& fb = *cached;
         std::vector<double> v;
         if (kind == 0) {

@@ -114,8 +114,9 @@ def extract_advanced_features_batch(images, as_numpy: bool = True):
     x = _device_planes(images)
     B, C, H, W = x.shape
     out = torch.empty((B * C, 18), dtype=torch.float64, device=x.device)
-    _lib.check_aux(_lib.load().wst_advanced_stats(x.data_ptr(), B * C, H, W, out.data_ptr(),
-                                                  torch.cuda.current_stream(x.device).cuda_stream))
+    with torch.cuda.device(x.device):
+        _lib.check_aux(_lib.load().wst_advanced_stats(x.data_ptr(), B * C, H, W, out.data_ptr(),
+                                                      torch.cuda.current_stream(x.device).cuda_stream))
     out = out.reshape(B, C * 18)
     return out.cpu().numpy() if as_numpy else out
 

@@ -76,7 +76,9 @@ def scatter_device(x, M, N, J, L, max_order, pre_pad, pooled=False, out=None):
     ws_bytes = plan.workspace_bytes(planes)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x.device)
     stream = torch.cuda.current_stream(x.device).cuda_stream
-    plan.forward(x.data_ptr(), B, out.data_ptr(), pooled, ws.data_ptr(), ws_bytes, stream)
+    # the plan is bound to x's device: make it current for the call (wst_forward checks it)
+    with torch.cuda.device(dev):
+        plan.forward(x.data_ptr(), B, out.data_ptr(), pooled, ws.data_ptr(), ws_bytes, stream)
     return out
 
 

@@ -73,9 +73,11 @@ def add_noise_batch(images, noise_type, intensity, seed=0, out="uint8_hwc"):
     B, H, W, C = t.shape
     o = _out(t, out)
     st = torch.cuda.current_stream(t.device).cuda_stream
-    _lib.check_aux(_lib.load().wst_noise_generate(_type_id(noise_type), float(intensity), t.data_ptr(),
-                                                  B, H, W, C, int(seed) & (2 ** 64 - 1),
-                                                  OUT_KINDS[out], o.data_ptr(), st))
+    with torch.cuda.device(t.device):
+        _lib.check_aux(_lib.load().wst_noise_generate(_type_id(noise_type), float(intensity),
+                                                      t.data_ptr(), B, H, W, C,
+                                                      int(seed) & (2 ** 64 - 1), OUT_KINDS[out],
+                                                      o.data_ptr(), st))
     return o
 
 
@@ -90,18 +92,21 @@ def apply_noise_draws(images, noise_type, intensity, draws, out="uint8_hwc"):
     st = torch.cuda.current_stream(t.device).cuda_stream
     tid = _type_id(noise_type)
     if tid == NOISE_TYPES["salt_and_pepper"]:
-        salt, pepper = (torch.as_tensor(np.ascontiguousarray(a, np.int32)).reshape(B, 2, -1).cuda()
-                        for a in draws)
+        salt, pepper = (torch.as_tensor(np.ascontiguousarray(a, np.int32)).reshape(B, 2, -1)
+                        .to(t.device) for a in draws)
         ns, npp = salt_pepper_counts(H, W, C, intensity)
         if salt.shape[-1] != ns or pepper.shape[-1] != npp:
             raise RuntimeError(f"salt/pepper counts must be {ns}/{npp}")
-        code = _lib.load().wst_noise_apply(tid, float(intensity), t.data_ptr(), B, H, W, C, None,
-                                           salt.data_ptr(), pepper.data_ptr(), OUT_KINDS[out],
-                                           o.data_ptr(), st)
+        with torch.cuda.device(t.device):
+            code = _lib.load().wst_noise_apply(tid, float(intensity), t.data_ptr(), B, H, W, C,
+                                               None, salt.data_ptr(), pepper.data_ptr(),
+                                               OUT_KINDS[out], o.data_ptr(), st)
     else:
-        d = torch.as_tensor(np.ascontiguousarray(draws, np.float64)).reshape(B, H, W, C).cuda()
-        code = _lib.load().wst_noise_apply(tid, float(intensity), t.data_ptr(), B, H, W, C,
-                                           d.data_ptr(), None, None, OUT_KINDS[out], o.data_ptr(), st)
+        d = torch.as_tensor(np.ascontiguousarray(draws, np.float64)).reshape(B, H, W, C).to(t.device)
+        with torch.cuda.device(t.device):
+            code = _lib.load().wst_noise_apply(tid, float(intensity), t.data_ptr(), B, H, W, C,
+                                               d.data_ptr(), None, None, OUT_KINDS[out],
+                                               o.data_ptr(), st)
     _lib.check_aux(code)
     return o
 

@@ -2,7 +2,13 @@
 
 Reference call sites: src/training/train_and_save_model.py:46,359,368 and
 src/visualization/visualize_features.py:30.  The array is staged to the GPU (H2D), transformed
-by the HIP library, and copied back (D2H).  Output dtype is float32 (the compute precision).
+by the HIP library, and copied back (D2H).
+
+Dtypes: the transform computes in float32 on the GPU.  A float64 input is rounded to float32 on
+the way in and the result is returned as float64 (same container dtype as the input, values
+carrying float32 precision); every other real input returns float32.  kymatio's numpy backend
+itself returns float64 for any input (its filters are float64); the
+reference casts its features to float64 afterwards anyway (train_and_save_model.py:371-378).
 """
 from __future__ import annotations
 
@@ -27,6 +33,8 @@ class Scattering2D(ScatteringBase2D):
         xd = torch.from_numpy(x).to("cuda", non_blocking=False)
         S = scatter_device(xd, self.M, self.N, self.J, self.L, self.max_order, self.pre_pad)
         S = S.cpu().numpy()
+        if input.dtype == np.float64:
+            S = S.astype(np.float64)
         S = S.reshape(batch_shape + S.shape[-3:])
         if self.out_type == "list":
             return self._to_list(S, batch_shape)
@@ -44,6 +52,7 @@ class Scattering2D(ScatteringBase2D):
         xd = torch.from_numpy(x).to("cuda")
         F = scatter_device(xd, self.M, self.N, self.J, self.L, self.max_order, self.pre_pad,
                            pooled=True)
-        return F.cpu().numpy().reshape(batch_shape + (2 * self.K,))
+        F = F.cpu().numpy().reshape(batch_shape + (2 * self.K,))
+        return F.astype(np.float64) if input.dtype == np.float64 else F
 
     __call__ = scattering
