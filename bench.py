@@ -333,7 +333,7 @@ def measure_probes(torch, lib, dev, stream):
     e1.synchronize()
     bw = 2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
     del src, dst
-    nthreads, iters = 256 * 2048, 4096
+    nthreads, iters = 256 * 2048, 2048
     scratch = torch.empty(nthreads, dtype=torch.float32, device=dev)
     _lib.check_aux(lib.wst_probe_fma(scratch.data_ptr(), nthreads, iters, stream))
     e0.record()
@@ -342,10 +342,10 @@ def measure_probes(torch, lib, dev, stream):
         _lib.check_aux(lib.wst_probe_fma(scratch.data_ptr(), nthreads, iters, stream))
     e1.record()
     e1.synchronize()
-    tf = 2.0 * 16 * iters * nthreads * reps / (e0.elapsed_time(e1) * 1e-3) / 1e12
+    tf = 2.0 * 32 * iters * nthreads * reps / (e0.elapsed_time(e1) * 1e-3) / 1e12
     return {"bw_gbs": round(bw, 1), "fp32_tflops": round(tf, 2),
-            "bw_probe": "16-B/lane non-temporal copy, 1 GiB -> 1 GiB, bytes read + written",
-            "fp32_probe": f"{nthreads} lanes x 16 independent v_fma_f32 chains x {iters} steps"}
+            "bw_probe": "16-B/lane streaming copy, 1 GiB -> 1 GiB, bytes read + written",
+            "fp32_probe": f"{nthreads} lanes x 32 independent v_fma_f32 chains x {iters} steps"}
 
 
 def launch_check(args, rank, world):

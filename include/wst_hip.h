@@ -217,8 +217,8 @@ int wst_u8_to_chw(const uint8_t* d_in, int64_t nimg, int H, int W, int C, float*
 
 /* Measurement probes for bench.py's measured rooflines (SURVEY.md §8(d) BW_meas / FP32_meas;
  * no kymatio counterpart): a 16-B-per-lane streaming copy of `bytes` (16-byte aligned), and
- * nthreads (multiple of 256) lanes each running 16 independent FMA chains for `iters` steps
- * (2 * 16 * iters FLOP per lane). */
+ * nthreads (multiple of 256) lanes each running 32 independent FMA chains for `iters` steps
+ * (2 * 32 * iters FLOP per lane). */
 int wst_probe_copy(const void* d_src, void* d_dst, size_t bytes, void* stream);
 int wst_probe_fma(float* d_scratch, int64_t nthreads, int iters, void* stream);
 

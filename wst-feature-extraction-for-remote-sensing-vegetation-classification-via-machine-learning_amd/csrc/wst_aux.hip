@@ -437,25 +437,35 @@ __global__ void k_u8_to_chw(const uint8_t* __restrict__ in, long long nimg, int 
 }
 
 // ---- measurement probes (bench.py: BW_meas, FP32_meas of SURVEY.md §8(d)) ----
-// Streaming copy, 16 B per lane per access, grid-stride.
+// Streaming copy, 16 B per lane per access, four accesses in flight per lane, grid-stride.
 typedef float v4f __attribute__((ext_vector_type(4)));
-__global__ void k_probe_copy(const v4f* __restrict__ src, v4f* __restrict__ dst, long long n) {
-    for (long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x; i < n;
-         i += static_cast<long long>(gridDim.x) * blockDim.x)
-        __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+__global__ void __launch_bounds__(256) k_probe_copy(const v4f* __restrict__ src, v4f* __restrict__ dst,
+                                                    long long n) {
+    const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
+    long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const v4f a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
 }
-// 16 independent FMA chains per lane; a, b are runtime values so nothing folds.
+// 32 independent FMA chains per lane, the step loop unrolled by 4 (loop overhead < 2 % of the
+// VALU issue); a, b are runtime values so nothing folds.
 __global__ void __launch_bounds__(256) k_probe_fma(float* out, int iters, float a, float b) {
-    float acc[16];
+    float acc[32];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) acc[k] = static_cast<float>(threadIdx.x + k);
+    for (int k = 0; k < 32; ++k) acc[k] = static_cast<float>(threadIdx.x + k);
+#pragma unroll 4
     for (int i = 0; i < iters; ++i) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) acc[k] = fmaf(acc[k], a, b);
+        for (int k = 0; k < 32; ++k) acc[k] = fmaf(acc[k], a, b);
     }
     float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) s += acc[k];
+    for (int k = 0; k < 32; ++k) s += acc[k];
     if (s == 1234.5f) out[blockIdx.x * blockDim.x + threadIdx.x] = s;   // never true: keeps the work
 }
 
@@ -584,7 +594,7 @@ int wst_probe_copy(const void* d_src, void* d_dst, size_t bytes, void* stream) {
         (reinterpret_cast<uintptr_t>(d_dst) & 15))
         return aux_fail(WST_ERR_INVALID, "copy probe needs 16-byte aligned buffers and size");
     const long long n = static_cast<long long>(bytes / 16);
-    hipLaunchKernelGGL(k_probe_copy, dim3(256 * 32), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL(k_probe_copy, dim3(256 * 16), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                        static_cast<const v4f*>(d_src), static_cast<v4f*>(d_dst), n);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return aux_fail(WST_ERR_HIP, hipGetErrorString(e));

@@ -84,6 +84,12 @@ struct DevParams {
     int box1_min_s;               // smallest order-1 alias count using the box-sparse fold
     const float* lpt;             // low-pass tap matrices in physical (digit-reversed) order:
     const int* lpt_off;           // [2r] GM_r (PM>>r rows x kLpOM), [2r+1] GN_r (PN>>r x oN)
+    // wide tap matrices for the MFMA low-pass (max(oM, oN) > kLpOM): GMw_r (PM>>r rows x oMp)
+    // and GNw_r (PN>>r rows x oNp), columns zero-padded to multiples of 16; [2r + d] in physical
+    // order (r < J), [2J + d] level 0 in natural order (k_prep)
+    const float* lpw;
+    const int* lpw_off;
+    int oMp, oNp;
 };
 
 // Per-launch LDS layout (byte offsets) and the table slices copied into LDS.
@@ -436,6 +442,104 @@ __device__ __forceinline__ void lds_lowpass(float2* U, int nb, int bs, int rows,
 }
 
 constexpr int kLpOM = 8;  // row stride of the GM tap matrices = largest oM of the fused path
+
+// Separable phi low-pass on the matrix cores (v_mfma_f32_16x16x4_f32: exact fp32, the fmaf chain
+// of the VALU form at the same rate, on the separate matrix pipe), for wide outputs
+// (max(oM, oN) > kLpOM: the reference's 128^2 J=2 geometry maps to 32 x 32, 64^2 J=2 to 16 x 16).
+// The low-pass at the kept output points is two small GEMMs per array b:
+//   1. T[p][c] = sum_q U[p][q] GN[q][c]      (rows x cols) . (cols x oNp), parked in the free .y
+//      slots of row p of U (c < oN);
+//   2. S[a][c] = sum_p GM[p][a] T[p][c]      (oMp x rows) . (rows x oNp)  -> S (nb x oM x oN).
+// U real in .x (row stride ld, array stride bs), in the physical order the tap matrices were
+// built for.  GM / GN: global (L2-resident) tap matrices, rows zero-padded to oMp / oNp (x16).
+// One wave per 16 x 16 output tile, K in steps of 4 x KU (loads of a step issued together, two
+// accumulators alternate so consecutive MFMAs do not wait on each other).  Lane map of the
+// 16x16x4 form: A[m = lane & 15][k = lane >> 4], B[k = lane >> 4][n = lane & 15],
+// D[row = 4 (lane >> 4) + i][col = lane & 15].  Ends with a barrier.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int rows, int cols, int ld,
+                                                 const float* __restrict__ GM,
+                                                 const float* __restrict__ GN, int oMp, int oNp,
+                                                 int oM, int oN, float* S) {
+    constexpr int KU = 4;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int nmt = (rows + 15) >> 4, nnt = oNp >> 4, nat = oMp >> 4;
+    // 1. T = U GN
+    const int ntask1 = nb * nmt * nnt;
+    for (int t = wave; t < ntask1; t += nw) {
+        const int b = t / (nmt * nnt);
+        const int r = t - b * nmt * nnt;
+        const int mt = r / nnt, nt = r - mt * nnt;
+        float2* Ub = U + b * bs;
+        const int p = mt * 16 + li;
+        const bool pok = p < rows;
+        const float2* urow = Ub + (pok ? p : rows - 1) * ld;
+        const float* gcol = GN + nt * 16 + li;
+        f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        for (int q0 = 0; q0 < cols; q0 += 4 * KU) {
+            float a[KU], bv[KU];
+#pragma unroll
+            for (int u = 0; u < KU; ++u) {
+                const int q = q0 + 4 * u + lk;
+                const bool ok = q < cols;
+                const int qc = ok ? q : 0;
+                a[u] = (ok && pok) ? urow[qc].x : 0.f;
+                bv[u] = ok ? gcol[qc * oNp] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < KU; u += 2) {
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[u], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u + 1], bv[u + 1], acc1, 0, 0, 0);
+            }
+        }
+        const int c = nt * 16 + li;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int pp = mt * 16 + lk * 4 + i;
+            if (pp < rows && c < oN) Ub[pp * ld + c].y = acc0[i] + acc1[i];
+        }
+    }
+    __syncthreads();
+    // 2. S = GM^T T
+    const int ntask2 = nb * nat * nnt;
+    for (int t = wave; t < ntask2; t += nw) {
+        const int b = t / (nat * nnt);
+        const int r = t - b * nat * nnt;
+        const int at = r / nnt, ct = r - at * nnt;
+        const float2* Ub = U + b * bs;
+        const int c = ct * 16 + li;
+        const bool cok = c < oN;
+        const float* gcol = GM + at * 16 + li;
+        f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        for (int p0 = 0; p0 < rows; p0 += 4 * KU) {
+            float a[KU], bv[KU];
+#pragma unroll
+            for (int u = 0; u < KU; ++u) {
+                const int pp = p0 + 4 * u + lk;
+                const bool ok = pp < rows;
+                const int pc = ok ? pp : 0;
+                a[u] = ok ? gcol[pc * oMp] : 0.f;
+                bv[u] = (ok && cok) ? Ub[pc * ld + c].y : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < KU; u += 2) {
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[u], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u + 1], bv[u + 1], acc1, 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int a_ = at * 16 + lk * 4 + i;
+            if (a_ < oM && cok) S[(b * oM + a_) * oN + c] = acc0[i] + acc1[i];
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ bool wide_lowpass(const DevParams& p) { return p.oM > kLpOM || p.oN > kLpOM; }
+__device__ __forceinline__ const float* lpw_M(const DevParams& p, int slot) { return p.lpw + p.lpw_off[2 * slot]; }
+__device__ __forceinline__ const float* lpw_N(const DevParams& p, int slot) { return p.lpw + p.lpw_off[2 * slot + 1]; }
 
 // Separable phi low-pass of one (rows x cols) real array (U[p][q].x, row stride ld) at the kept
 // output points through the level's tap matrices (physical order, unpad and decimation folded in;
@@ -1046,7 +1150,10 @@ __device__ __forceinline__ void prep_body(unsigned char* smem, const DevParams& 
     const float mean = block_sum(part, red) / n;  // contains the barrier after the gather
 
     // S0: low-pass at level 0, decimation 2^J
-    lds_lowpass(A, 1, 0, PM, PN, ld, tb.lpM(0), tb.lpN(0), nullptr, nullptr, 1 << p.J, p.oM, p.oN, S);
+    if (wide_lowpass(p))   // natural-order level-0 tap matrices (slot J)
+        lds_lowpass_mfma(A, 1, 0, PM, PN, ld, lpw_M(p, p.J), lpw_N(p, p.J), p.oMp, p.oNp, p.oM, p.oN, S);
+    else
+        lds_lowpass(A, 1, 0, PM, PN, ld, tb.lpM(0), tb.lpN(0), nullptr, nullptr, 1 << p.J, p.oM, p.oN, S);
     emit(S, 1, 0, img, p.K, p.oM, p.oN, out, pooled);
 
     // mean-centred forward DFT for the band-pass paths (.y reset: the low-pass parked sums there)
@@ -1139,6 +1246,9 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     if (!(dbg & 2)) {
         if constexpr (SQ)
             lds_lowpass_taps<8, 16>(A, nM1, nN1, ld1, tb.gM(j1), tb.gN(j1), oms, oM, oN, S);
+        else if (wide_lowpass(p))
+            lds_lowpass_mfma(A, 1, 0, nM1, nN1, ld1, lpw_M(p, j1), lpw_N(p, j1), p.oMp, p.oNp, oM,
+                             oN, S);
         else
             lds_lowpass(A, 1, 0, nM1, nN1, ld1, tb.lpM(j1), tb.lpN(j1), tb.pmM(j1), tb.pmN(j1),
                         1 << (J - j1), oM, oN, S);
@@ -1284,7 +1394,11 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                     lds_fft2<FM, FN, 0, MAXN, kDR, true>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
                                                          tb.twN(j2), mod2);
                 if (!(dbg & 64)) {
-                    lds_lowpass(B, npath, pslot, nM2, nN2, ld2, tb.lpM(j2), tb.lpN(j2), tb.pmM(j2),
+                    if (wide_lowpass(p))
+                        lds_lowpass_mfma(B, npath, pslot, nM2, nN2, ld2, lpw_M(p, j2), lpw_N(p, j2),
+                                         p.oMp, p.oNp, oM, oN, S);
+                    else
+                        lds_lowpass(B, npath, pslot, nM2, nN2, ld2, tb.lpM(j2), tb.lpN(j2), tb.pmM(j2),
                                 tb.pmN(j2), 1 << (J - j2), oM, oN, S);
                     emit(S, npath, kbase + (j2 - j1 - 1) * L + l2a, img, p.K, oM, oN, out, pooled);
                 }

@@ -160,6 +160,8 @@ struct wst_plan {
     std::vector<const wstlaunch::BigOps*> big;    // per staged level
     std::vector<int> lpn_off;                     // natural tap matrices: [2r] GM_r, [2r+1] GN_r
     float* d_lpn = nullptr;
+    float* d_lpw = nullptr;                       // wide tap matrices (MFMA low-pass)
+    int* d_lpw_off = nullptr;
     std::vector<LdsLayout> hg_lay;                // k_o2 (global spectrum) after a staged j1
     std::vector<size_t> hg_lds;
     std::vector<int> hg_threads, hg_j2first;
@@ -204,6 +206,8 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_lpt);
     (void)hipFree(p->d_lpt_off);
     (void)hipFree(p->d_lpn);
+    (void)hipFree(p->d_lpw);
+    (void)hipFree(p->d_lpw_off);
     for (auto& kv : p->ws_by_stream)
         if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     delete p;
@@ -546,6 +550,26 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                     lpn.push_back(a < no ? static_cast<float>(h[((sdec * (a + 1) - p) % n + n) % n]) : 0.f);
         }
     plan->oms = oms;
+    // wide tap matrices for the MFMA low-pass (lds_lowpass_mfma), columns padded to x16:
+    //   [2r + d] level r in physical order (r < J), [2J + d] level 0 in natural order (k_prep)
+    const int oMp = (g.oM + 15) & ~15, oNp = (g.oN + 15) & ~15;
+    std::vector<float> lpw;
+    std::vector<int> lpw_off(2 * static_cast<size_t>(J + 1), 0);
+    for (int slot = 0; slot <= J; ++slot)
+        for (int d = 0; d < 2; ++d) {
+            const int r = slot < J ? slot : 0;
+            const int n = (d == 0 ? g.PM : g.PN) >> r;
+            const int no = d == 0 ? g.oM : g.oN, np_ = d == 0 ? oMp : oNp;
+            const int sdec = 1 << (J - r);
+            const auto& h = d == 0 ? fb.hM[r] : fb.hN[r];
+            const int* pm = perm.data() + t.perm_off[2 * r + d];
+            lpw_off[2 * slot + d] = static_cast<int>(lpw.size());
+            for (int q = 0; q < n; ++q) {
+                const int phys = slot < J ? pm[q] : q;
+                for (int a = 0; a < np_; ++a)
+                    lpw.push_back(a < no ? static_cast<float>(h[((sdec * (a + 1) - phys) % n + n) % n]) : 0.f);
+            }
+        }
     // twiddles exp(-2 pi i k / n) per level and side; pool order: M levels 0..J, then N levels
     std::vector<float2> tw;
     t.tw_off.assign(2 * static_cast<size_t>(J + 1) + 1, 0);
@@ -591,6 +615,8 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     if ((rc = upload(&plan->d_lpt, lpt)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_lpt_off, t.lpt_off)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_lpn, lpn)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_lpw, lpw)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_lpw_off, lpw_off)) != WST_OK) return rc;
 
     DevParams& dp = plan->dp;
     dp.M = g.M; dp.N = g.N; dp.PM = g.PM; dp.PN = g.PN; dp.J = J; dp.L = L;
@@ -614,6 +640,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     dp.box1_min_s = 8;
     if (const char* e = diag_env("WST_BOX1_MIN_S")) dp.box1_min_s = std::atoi(e);
     dp.lpt = plan->d_lpt; dp.lpt_off = plan->d_lpt_off;
+    dp.lpw = plan->d_lpw; dp.lpw_off = plan->d_lpw_off; dp.oMp = oMp; dp.oNp = oNp;
     // square variant (bounded FFT sizes + fused order-2 low-pass): square plane of a compiled
     // family, oM <= kLpOM and every order-2 level's column units hold ceil(oM / 2) slots
     plan->sq = (plan->fam_m > 0 && plan->fam_m == plan->fam_n && g.PM == g.PN &&
