@@ -90,6 +90,13 @@ struct DevParams {
     const float* lpw;
     const int* lpw_off;
     int oMp, oNp;
+    // natural-order tap matrices ([2r] GM_r, [2r+1] GN_r; rows of oms floats) and the single-path
+    // order-2 filters of the first order-2 level (psi_{j1+1,l2} at level j1, N1 x N1 floats,
+    // [j1*L + l2], -1 where not built): k_o2w (wst_wave.h)
+    const float* lpn;
+    const int* lpn_off;
+    const float* psi2s;
+    const long long* psi2s_off;
 };
 
 // Per-launch LDS layout (byte offsets) and the table slices copied into LDS.
@@ -1413,7 +1420,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             constexpr int k = decltype(kc)::value;
             constexpr int NN2 = N1C >> k;
             if constexpr ((NN2 << k) == N1C && NN2 >= 1)
-                if (j1 + k < J) level(j1 + k, NN2, NN2);
+                if (j1 + k < J && j1 + k >= j2first) level(j1 + k, NN2, NN2);
         });
     } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {
         // after a big level the paths start at the first LDS-resident level, which is the
