@@ -90,13 +90,6 @@ struct DevParams {
     const float* lpw;
     const int* lpw_off;
     int oMp, oNp;
-    // natural-order tap matrices ([2r] GM_r, [2r+1] GN_r; rows of oms floats) and the single-path
-    // order-2 filters of the first order-2 level (psi_{j1+1,l2} at level j1, N1 x N1 floats,
-    // [j1*L + l2], -1 where not built): k_o2w (wst_wave.h)
-    const float* lpn;
-    const int* lpn_off;
-    const float* psi2s;
-    const long long* psi2s_off;
 };
 
 // Per-launch LDS layout (byte offsets) and the table slices copied into LDS.

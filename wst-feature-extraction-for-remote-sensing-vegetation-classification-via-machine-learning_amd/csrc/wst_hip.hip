@@ -162,12 +162,6 @@ struct wst_plan {
     float* d_lpn = nullptr;
     float* d_lpw = nullptr;                       // wide tap matrices (MFMA low-pass)
     int* d_lpw_off = nullptr;
-    int* d_lpn_off = nullptr;
-    float* d_psi2s = nullptr;                     // single-path first-level order-2 filters (k_o2w)
-    long long* d_psi2s_off = nullptr;
-    std::vector<int> o2w;                         // per j1: order 2 through k_o2w (wst_wave.h)
-    std::vector<LdsLayout> o2w_lay;
-    std::vector<size_t> o2w_lds;
     std::vector<LdsLayout> hg_lay;                // k_o2 (global spectrum) after a staged j1
     std::vector<size_t> hg_lds;
     std::vector<int> hg_threads, hg_j2first;
@@ -214,9 +208,6 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_lpn);
     (void)hipFree(p->d_lpw);
     (void)hipFree(p->d_lpw_off);
-    (void)hipFree(p->d_lpn_off);
-    (void)hipFree(p->d_psi2s);
-    (void)hipFree(p->d_psi2s_off);
     for (auto& kv : p->ws_by_stream)
         if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     delete p;
@@ -457,20 +448,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                     }
                 }
     }
-    // single-path copies of the first order-2 level's filters (psi_{j1+1,l2} at level j1) for the
-    // levels whose paths k_o2w folds one per wave (n1 / 2 in (32, 64], square planes)
-    std::vector<float> psi2s;
-    std::vector<long long> psi2s_off(static_cast<size_t>(J) * L, -1);
-    if (max_order >= 2 && g.PM == g.PN) {
-        for (int j1 = 0; j1 + 1 < J; ++j1) {
-            const int n1 = g.PM >> j1;
-            if (!wstdev::o2w_reg(n1, n1 / 2) || (n1 / 2) * 2 != n1 || j1 >= wst::psi_levels(j1 + 1, J)) continue;
-            for (int l2 = 0; l2 < L; ++l2) {
-                psi2s_off[static_cast<size_t>(j1) * L + l2] = static_cast<long long>(psi2s.size());
-                for (double v : fb.psi[static_cast<size_t>(j1 + 1) * L + l2][j1]) psi2s.push_back(static_cast<float>(v));
-            }
-        }
-    }
     // alias boxes of the order-2 pairs (see fold2): per (j2, r) all pairs, stride nM2 + nN2
     std::vector<int> box;
     std::vector<int> box_off(static_cast<size_t>(J) * J, 0);
@@ -640,9 +617,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     if ((rc = upload(&plan->d_lpn, lpn)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_lpw, lpw)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_lpw_off, lpw_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_lpn_off, plan->lpn_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_psi2s, psi2s)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_psi2s_off, psi2s_off)) != WST_OK) return rc;
 
     DevParams& dp = plan->dp;
     dp.M = g.M; dp.N = g.N; dp.PM = g.PM; dp.PN = g.PN; dp.J = J; dp.L = L;
@@ -667,8 +641,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     if (const char* e = diag_env("WST_BOX1_MIN_S")) dp.box1_min_s = std::atoi(e);
     dp.lpt = plan->d_lpt; dp.lpt_off = plan->d_lpt_off;
     dp.lpw = plan->d_lpw; dp.lpw_off = plan->d_lpw_off; dp.oMp = oMp; dp.oNp = oNp;
-    dp.lpn = plan->d_lpn; dp.lpn_off = plan->d_lpn_off;
-    dp.psi2s = plan->d_psi2s; dp.psi2s_off = plan->d_psi2s_off;
     // square variant (bounded FFT sizes + fused order-2 low-pass): square plane of a compiled
     // family, oM <= kLpOM and every order-2 level's column units hold ceil(oM / 2) slots
     plan->sq = (plan->fam_m > 0 && plan->fam_m == plan->fam_n && g.PM == g.PN &&
@@ -815,26 +787,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                                       smax);
         if (plan->o2_lds[j1] > static_cast<size_t>(kMaxLds)) return too_big("k_o2", j1);
     }
-    // k_o2w (wst_wave.h): the first order-2 level of square planes of a compiled family with 4 x 4
-    // output maps, one path per wave (L <= 8), when a lane can own a line (n1 / 2 in 33..64); the
-    // block holds the level's half spectrum, later reused as the waves' transposition buffers
-    plan->o2w.assign(J, 0);
-    plan->o2w_lay.assign(J, LdsLayout{});
-    plan->o2w_lds.assign(J, 0);
-    bool o2w_on = true;
-    if (const char* e = diag_env("WST_O2W")) o2w_on = std::atoi(e) != 0;
-    for (int j1 = plan->rb; j1 + 1 < J && max_order >= 2; ++j1) {
-        const int n1 = g.PM >> j1;
-        if (!o2w_on || !plan->sq || g.PM != g.PN || g.oM != 4 || g.oN != 4 || oms != 4 ||
-            L > wstdev::kO2wWaves || !wstdev::o2w_supported(plan->fam_m, n1) ||
-            psi2s_off[static_cast<size_t>(j1) * L] < 0)
-            continue;
-        const size_t hbytes = static_cast<size_t>(n1) * (n1 / 2 + 1) * sizeof(float2);
-        const size_t wbytes = static_cast<size_t>(wstdev::kO2wWaves) * wstdev::o2w_wave_floats(n1) * sizeof(float);
-        plan->o2w_lds[j1] = layout(plan->o2w_lay[j1], std::max(hbytes, wbytes), 0, t, Blocks{j1, j1, false}, 1,
-                                   0, static_cast<size_t>(n1 / 2) * oms, Blocks{}, oms);
-        plan->o2w[j1] = plan->o2w_lds[j1] <= static_cast<size_t>(kMaxLds);
-    }
     plan->ws_plane = align16(wsp);
     if (plan->rb > 0)   // staged plans hold ~tens of MB per plane: bound the chunk to ~2 GB
         plan->max_chunk = std::max<int64_t>(1, std::min<int64_t>(2048, (size_t(2) << 30) / plan->ws_plane));
@@ -842,9 +794,9 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         std::fprintf(stderr, "[wst] plan %dx%d J=%d L=%d P=%dx%d fam=(%d,%d) sq=%d prep_lds=%zu\n", M, N, J, L,
                      g.PM, g.PN, plan->fam_m, plan->fam_n, plan->sq, plan->prep_lds);
         for (int j1 = 0; j1 < J; ++j1)
-            std::fprintf(stderr, "[wst]   j1=%d cap=%d o1: %d thr %zu B   o2: %d thr %zu B   o2w: %d (%zu B)\n", j1,
+            std::fprintf(stderr, "[wst]   j1=%d cap=%d o1: %d thr %zu B   o2: %d thr %zu B\n", j1,
                          plan->cap[j1], plan->o1_threads[j1], plan->o1_lds[j1], plan->o2_threads[j1],
-                         plan->o2_lds[j1], plan->o2w[j1], plan->o2w_lds[j1]);
+                         plan->o2_lds[j1]);
     }
     for (int j1 = plan->rb; j1 < J; ++j1) {
         plan->o1_threads[j1] = fill_cu(plan->o1_threads[j1], plan->o1_lds[j1]);
@@ -951,18 +903,9 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
     if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
     if (!do2) return WST_OK;
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
-    int j2first = j1 + 1;
-    if (plan->o2w[j1]) {   // level j1 + 1 through k_o2w, the smaller levels through k_o2
-        const Launch q{dim3(nimg * g.L), dim3(64 * wstdev::kO2wWaves), plan->o2w_lds[j1], stream};
-        if (!plan->ops->o2w(g.PM >> j1, q, plan->dp, plan->o2w_lay[j1], j1, nimg, img0, hexp, d_out, pooled))
-            return fail(WST_ERR_UNSUPPORTED, "k_o2w not compiled for level size " + std::to_string(g.PM >> j1));
-        WST_HIP_CHECK(hipGetLastError());
-        j2first = j1 + 2;
-    }
-    if (j2first < g.J)
-        plan->ops->o2(plan->cap[j1], plan->sq, 0,
-                      Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
-                      plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j2first);
+    plan->ops->o2(plan->cap[j1], plan->sq, 0,
+                  Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
+                  plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j1 + 1);
     WST_HIP_CHECK(hipGetLastError());
     return timer.end(stream, 1 + g.J + j1);
 }

@@ -32,50 +32,12 @@ hipError_t attrs_all() {
     return attrs_cap<136, SQ>();
 }
 
-// k_o2w instantiations of a square family: level sizes FM * 2^k (wstdev::o2w_supported)
-template <int K>
-hipError_t attrs_o2w() {
-    if constexpr (K <= 7) {
-        constexpr int N1C = FM << K;
-        if constexpr (kSquareFamily && wstdev::o2w_supported(FM, N1C)) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2w<FM, N1C>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds);
-            if (e != hipSuccess) return e;
-        }
-        return attrs_o2w<K + 1>();
-    }
-    return hipSuccess;
-}
-
-template <int K>
-bool o2w_k(int n1c, const Launch& q, const DevParams& dp, const LdsLayout& lay, int j1, int nimg,
-           long long img0, const float2* hexp, float* out, int pooled) {
-    if constexpr (K <= 7) {
-        constexpr int N1C = FM << K;
-        if constexpr (kSquareFamily && wstdev::o2w_supported(FM, N1C)) {
-            if (n1c == N1C) {
-                hipLaunchKernelGGL((wstdev::k_o2w<FM, N1C>), q.grid, q.block, q.lds, q.st, dp, lay, j1,
-                                   nimg, img0, hexp, out, pooled);
-                return true;
-            }
-        }
-        return o2w_k<K + 1>(n1c, q, dp, lay, j1, nimg, img0, hexp, out, pooled);
-    }
-    return false;
-}
-
-bool o2w(int n1c, const Launch& q, const DevParams& dp, const LdsLayout& lay, int j1, int nimg,
-         long long img0, const float2* hexp, float* out, int pooled) {
-    return o2w_k<0>(n1c, q, dp, lay, j1, nimg, img0, hexp, out, pooled);
-}
-
 hipError_t set_attrs() {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_prep<FM, FN>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds);
     if (e != hipSuccess) return e;
     if ((e = attrs_all<0>()) != hipSuccess) return e;
     if constexpr (kSquareFamily) {
-        if ((e = attrs_o2w<0>()) != hipSuccess) return e;
         if ((e = attrs_all<1>()) != hipSuccess) return e;
         return hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2<FM, FN, 136, 1, 1>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds);
@@ -140,7 +102,7 @@ void o2(int cap, int sq, int hg, const Launch& q, const DevParams& dp, const Lds
 #define WST_GETTER_NAME(A, B) WST_FAMILY_GETTER(A, B)
 #define WST_GETTER_EXPAND(A, B) WST_GETTER_NAME(A, B)
 const FamilyOps& WST_GETTER_EXPAND(WST_FAM_M, WST_FAM_N)() {
-    static const FamilyOps ops{FM, FN, set_attrs, prep, o1, o2, o2w};
+    static const FamilyOps ops{FM, FN, set_attrs, prep, o1, o2};
     return ops;
 }
 

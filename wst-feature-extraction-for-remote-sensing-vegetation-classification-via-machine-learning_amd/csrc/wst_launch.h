@@ -7,7 +7,6 @@
 
 #include "wst_device.h"
 #include "wst_staged.h"
-#include "wst_wave.h"
 
 namespace wstlaunch {
 
@@ -32,10 +31,6 @@ struct FamilyOps {
     // hg: spectrum of a big level read from HBM (square families, cap 136), paths from j2first
     void (*o2)(int cap, int sq, int hg, const Launch&, const DevParams&, const LdsLayout&, int j1,
                int nimg, long long img0, const float2* hexp, float* out, int pooled, int j2first);
-    // wave-per-path order-2 kernel k_o2w at level size n1c (wst_wave.h); false when this family
-    // has no instantiation for n1c (the caller then launches o2)
-    bool (*o2w)(int n1c, const Launch&, const DevParams&, const LdsLayout&, int j1, int nimg,
-                long long img0, const float2* hexp, float* out, int pooled);
 };
 
 // HBM-staged passes of one big level size N (wst_staged.h), compiled per N (wst_staged.hip).
