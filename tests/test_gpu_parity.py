@@ -91,9 +91,12 @@ def test_training_and_inference_feature_layouts():
     np.testing.assert_array_equal(g.reshape(3, 81, 2), np.moveaxis(got, 1, 2))
 
 
-def test_pooled_equals_pooling_of_full_output():
-    x = rgb(5, (16, 3, 64, 64))
-    s = ThS(J=4, shape=(64, 64), L=8)
+@pytest.mark.parametrize("M,J", [(64, 4),     # 4 x 4 maps: one thread per map
+                                 (64, 2),     # 16 x 16: one wave per map
+                                 (128, 2)])   # 32 x 32: the reference's training geometry
+def test_pooled_equals_pooling_of_full_output(M, J):
+    x = rgb(5, (16 if M == 64 else 4, 3, M, M))
+    s = ThS(J=J, shape=(M, M), L=8)
     xt = torch.from_numpy(x).cuda()
     S = s(xt).double()
     P = s.pooled(xt).double()
