@@ -119,11 +119,11 @@ def staged_levels(PM, PN, J):
 
 
 def family(P):
-    """FFT size family of a padded size: its odd part when compiled (1, 3, 5, 9, 17), else 0."""
+    """FFT size family of a padded size: its odd part when compiled, else 0 (generic DFT)."""
     o = P
     while o % 2 == 0:
         o //= 2
-    return o if o in (1, 3, 5, 9, 17) else 0
+    return o if o in (1, 3, 5, 7, 9, 11, 13, 15, 17, 27) else 0
 
 
 def rocprof_name(slot, PM, PN, J):

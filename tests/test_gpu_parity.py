@@ -201,12 +201,19 @@ def test_full_size_c2_properties_and_sampled_oracle():
 
 
 # Geometries whose SQ kernels run with compile-time level sizes for families other than the
-# headline's 3 (wst_device.h unique_level), a family-1 plane (two sizes per class: runtime sizes)
-# and a family-7 plane (generic DFT), each against the float64 oracle computed here.
+# headline's 3 (wst_device.h unique_level), a family-1 plane (two sizes per class: runtime sizes),
+# the families of common patch sizes (7, 11, 13, 15, 27) and a family-19 plane (generic DFT), each
+# against the float64 oracle computed here.
 @pytest.mark.parametrize("M,J,L", [(48, 4, 8),    # P = 80 (family 5): 80 / 40 / 20 compile-time
                                    (56, 3, 6),    # P = 72 (family 9): 72 / 36 / 18 compile-time
                                    (48, 3, 8),    # P = 64 (family 1): 64 and 128 share a class
-                                   (40, 3, 8)])   # P = 56 (family 7): generic DFT
+                                   (40, 3, 8),    # P = 56 (family 7)
+                                   (48, 2, 8),    # P = 56 (family 7): 16 x 16 maps (wide low-pass)
+                                   (80, 2, 4),    # P = 88 (family 11)
+                                   (96, 2, 4),    # P = 104 (family 13)
+                                   (112, 2, 4),   # P = 120 (family 15)
+                                   (100, 2, 4),   # P = 108 (family 27)
+                                   (68, 2, 4)])   # P = 76 (family 19): generic DFT
 def test_family_geometries_against_oracle(M, J, L):
     x = rgb(7 + M + J, (2, M, M))
     got = NpS(J=J, shape=(M, M), L=L)(x)

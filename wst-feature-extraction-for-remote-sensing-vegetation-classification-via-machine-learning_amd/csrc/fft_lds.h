@@ -24,10 +24,13 @@
 
 // Every level size of a plan is odd * 2^k (P = (M/2^J + 2) * 2^J), so kernels are instantiated
 // per "size family" (the odd part of P) and compile only that family's FFTs (kMaxFamilyN bounds
-// the LDS-resident sizes).  Families with compiled FFTs: 1, 3, 5, 9, 17 (others: generic DFT).
+// the LDS-resident sizes).  Families with compiled FFTs: 1, 3, 5, 7, 9, 11, 13, 15, 17, 27 (the
+// odd parts of P for the common patch sizes: 48 -> 56 = 7 x 8 at J = 2, 96 -> 104 = 13 x 8,
+// 112 -> 120 = 15 x 8, 100 -> 108 = 27 x 4 ...; others: generic DFT).
 #define WST_FFT_SIZES(X) \
-    X(2) X(3) X(4) X(5) X(6) X(8) X(9) X(10) X(12) X(16) X(17) X(18) X(20) X(24) X(32) X(34) \
-    X(36) X(40) X(48) X(64) X(68) X(72) X(80) X(96) X(128) X(136)
+    X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18)  \
+    X(20) X(22) X(24) X(26) X(27) X(28) X(30) X(32) X(34) X(36) X(40) X(44) X(48) X(52) X(54)      \
+    X(56) X(60) X(64) X(68) X(72) X(80) X(88) X(96) X(104) X(108) X(112) X(120) X(128) X(136)
 
 namespace wstfft {
 

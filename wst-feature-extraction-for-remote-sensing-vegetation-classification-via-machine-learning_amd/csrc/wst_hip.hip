@@ -56,7 +56,8 @@ int odd_part(int n) {
 }
 int family_of(int P) {
     const int o = odd_part(P);
-    const bool compiled = (o == 1 || o == 3 || o == 5 || o == 9 || o == 17);
+    const bool compiled = (o == 1 || o == 3 || o == 5 || o == 7 || o == 9 || o == 11 || o == 13 ||
+                           o == 15 || o == 17 || o == 27);
     return compiled ? o : 0;
 }
 const wstlaunch::BigOps* big_ops(int n) {

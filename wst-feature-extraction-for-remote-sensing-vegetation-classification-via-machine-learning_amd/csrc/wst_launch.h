@@ -57,7 +57,9 @@ struct BigCommonOps {
 const BigCommonOps& wst_big_common_ops();
 
 // The compiled family pairs (rows, columns); family 0 = generic O(n) DFT.
-#define WST_FAMILY_PAIRS(X) X(0, 0) X(1, 1) X(3, 3) X(5, 5) X(9, 9) X(17, 17) X(3, 1) X(1, 3)
+#define WST_FAMILY_PAIRS(X) \
+    X(0, 0) X(1, 1) X(3, 3) X(5, 5) X(7, 7) X(9, 9) X(11, 11) X(13, 13) X(15, 15) X(17, 17) X(27, 27) \
+    X(3, 1) X(1, 3)
 #define WST_FAMILY_GETTER(A, B) wst_family_ops_##A##_##B
 #define WST_DECLARE_GETTER(A, B) const FamilyOps& WST_FAMILY_GETTER(A, B)();
 WST_FAMILY_PAIRS(WST_DECLARE_GETTER)
