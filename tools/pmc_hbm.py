@@ -10,7 +10,7 @@ def per_kernel(d, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            m = re.search(r"(k_[a-z0-9]+<[^>]*>)", r["Kernel_Name"])
+            m = re.search(r"(k_[a-z0-9_]+<[^>]*>|k_big_[a-z]+)", r["Kernel_Name"])
             if m:
                 vals[m.group(1)].append(float(r["Counter_Value"]))
     return vals

@@ -75,7 +75,16 @@ const FamilyOps* family_ops(int fm, int fn) {
     return nullptr;
 }
 int cap_for(int n) { return n <= 12 ? 12 : n <= 24 ? 24 : n <= 48 ? 48 : 136; }
-constexpr int kBigRows = 8;   // rows per row-pass workgroup of the staged levels
+constexpr int kBigRows = 8;   // rows per row-pass workgroup of the staged levels (kRowFold2: 2 paths)
+// Rows per row-pass workgroup by mode: the LDS holds 2 kBigRows lines, so the single-path modes
+// take 2 kBigRows rows and kRowReal2 (two rows per complex line) 4 kBigRows, when n allows: at
+// n = 384 the 8-line FFT stages left half the 256 threads idle (kRowReal2: three quarters).
+int big_rows(int mode, int n) {
+    const int want = mode == wstbig::kRowFold2 ? kBigRows : mode == wstbig::kRowReal2 ? 4 * kBigRows : 2 * kBigRows;
+    for (int r = want; r > kBigRows; r /= 2)
+        if (n % r == 0) return r;
+    return kBigRows;
+}
 
 size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
 
@@ -938,7 +947,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         a.mode = mode;
         a.n = PM >> r;
         a.lvl = r;
-        a.rows = kBigRows;
+        a.rows = big_rows(mode, PM >> r);
         a.ncols = PM >> r;
         a.L = L;
         a.img0 = img0;
@@ -956,7 +965,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         a.tpart = part;
         a.gnat = gnat(0, 1);
         a.dst = xhat;
-        plan->big[0]->rows(false, Launch{dim3(PM / kBigRows, nimg), tb, plan->big_rows_lds[0], stream}, dp, a);
+        plan->big[0]->rows(false, Launch{dim3(PM / a.rows, nimg), tb, plan->big_rows_lds[0], stream}, dp, a);
         BigArgs c = args(kColStore, 0);
         c.dst = xhat;
         plan->big[0]->cols(false, Launch{dim3((PM + kColTile - 1) / kColTile, nimg), tb, plan->big_cols_lds[0], stream},
@@ -978,7 +987,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         a.xhat = xhat;
         a.j1 = j1;
         a.dst = tmp;
-        B1->rows(true, Launch{dim3(n1 / kBigRows, nimg * L), tb, plan->big_rows_lds[j1], stream}, dp, a);
+        B1->rows(true, Launch{dim3(n1 / a.rows, nimg * L), tb, plan->big_rows_lds[j1], stream}, dp, a);
         BigArgs c = args(kColModLp, j1);
         c.dst = tmp;
         c.uout = do2 ? ureal : nullptr;
@@ -996,7 +1005,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
             r2.ureal = ureal;
             r2.mean = umean;
             r2.dst = hbig;
-            B1->rows(false, Launch{dim3(n1 / kBigRows, nimg * L), tb, plan->big_rows_lds[j1], stream}, dp, r2);
+            B1->rows(false, Launch{dim3(n1 / r2.rows, nimg * L), tb, plan->big_rows_lds[j1], stream}, dp, r2);
             BigArgs c2 = args(kColStore, j1);
             c2.ncols = hld;
             c2.dst = hbig;
@@ -1023,7 +1032,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
                 f.npair = nq;
                 f.npath = L;
                 f.dst = tmp;
-                B2->rows(true, Launch{dim3(n2 / kBigRows, nimg), tb, plan->big_rows_lds[j2], stream}, dp, f);
+                B2->rows(true, Launch{dim3(n2 / f.rows, nimg), tb, plan->big_rows_lds[j2], stream}, dp, f);
                 BigArgs m2 = args(kColModLp, j2);
                 m2.dst = tmp;
                 m2.vpart = part;

@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
                 float2* D = a.dst + (static_cast<long long>(arr) * a.npath + path) * N * N;
                 for (int i = threadIdx.x; i < a.rows * N; i += T) {
                     const int rr = i / N, q = i - (i / N) * N;
-                    D[(r0 + rr) * N + q] = A[(b * a.rows + rr) * ld + q];
+                    wstdev::stnt(D + (r0 + rr) * N + q, A[(b * a.rows + rr) * ld + q]);
                 }
             }
             __syncthreads();
@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
         float2* D = a.dst + static_cast<long long>(arr) * N * N;
         for (int i = threadIdx.x; i < a.rows * N; i += T) {
             const int rr = i / N, q = i - (i / N) * N;
-            D[(r0 + rr) * N + q] = A[rr * ld + q];
+            wstdev::stnt(D + (r0 + rr) * N + q, A[rr * ld + q]);
         }
     } else if (a.mode == kRowReal2) {
         constexpr int hld = N / 2 + 1;
@@ -216,8 +216,8 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
             const float2 z = A[t * ld + q];
             const float2 zm = A[t * ld + (q == 0 ? 0 : N - q)];
             const int u = r0 + 2 * t;
-            D[u * hld + q] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
-            D[(u + 1) * hld + q] = make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
+            wstdev::stnt(D + u * hld + q, make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y)));
+            wstdev::stnt(D + (u + 1) * hld + q, make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x)));
         }
     }
 }
@@ -241,7 +241,7 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
     float2* src = a.dst + static_cast<long long>(arr) * N * a.ncols;
     for (int i = threadIdx.x; i < N * C; i += T) {
         const int u = i / C, c = i - (i / C) * C;
-        if (c < nc) A[c * ld + u] = src[static_cast<long long>(u) * a.ncols + c0 + c];
+        if (c < nc) A[c * ld + u] = wstdev::ldnt(src + static_cast<long long>(u) * a.ncols + c0 + c);
     }
     __syncthreads();
     if (a.mode == kColStore) {
@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
         wstfft::fft_lines<N, INV>(A, wstfft::Lines(1, 0, nc, ld, 1), tw, id);
         for (int i = threadIdx.x; i < N * C; i += T) {
             const int u = i / C, c = i - (i / C) * C;
-            if (c < nc) src[static_cast<long long>(u) * a.ncols + c0 + c] = A[c * ld + u];
+            if (c < nc) wstdev::stnt(src + static_cast<long long>(u) * a.ncols + c0 + c, A[c * ld + u]);
         }
         return;
     }
