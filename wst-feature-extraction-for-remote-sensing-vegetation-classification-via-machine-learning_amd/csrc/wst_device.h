@@ -104,6 +104,8 @@ struct LdsLayout {
     int oms;                // row stride of the tap matrices (4 or kLpOM)
     int off_s, off_red;     // S (coefficients) and reduction scratch
     int bcap;               // complex capacity of B (k_o2)
+    int export_full;        // k_o1: export the fully transformed half spectra (natural order) for a
+                            // k_o2 that folds from HBM (HG = 1) instead of the row-transformed ones
 };
 
 // ------------------------------------------------------------------------------------------
@@ -457,10 +459,13 @@ constexpr int kLpOM = 8;  // row stride of the GM tap matrices = largest oM of t
 // 16x16x4 form: A[m = lane & 15][k = lane >> 4], B[k = lane >> 4][n = lane & 15],
 // D[row = 4 (lane >> 4) + i][col = lane & 15].  Ends with a barrier.
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+// S addressing: map b, value i = a * oN + c at S[b * s_bs + i * s_es] (default: contiguous maps;
+// k_o2 passes the .x slots of the arrays U themselves, free once step 1 has read them).
 __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int rows, int cols, int ld,
                                                  const float* __restrict__ GM,
                                                  const float* __restrict__ GN, int oMp, int oNp,
-                                                 int oM, int oN, float* S) {
+                                                 int oM, int oN, float* S, int s_bs = -1, int s_es = 1) {
+    if (s_bs < 0) s_bs = oM * oN;
     constexpr int KU = 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int li = lane & 15, lk = lane >> 4;
@@ -531,7 +536,7 @@ __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int a_ = at * 16 + lk * 4 + i;
-            if (a_ < oM && cok) S[(b * oM + a_) * oN + c] = acc0[i] + acc1[i];
+            if (a_ < oM && cok) S[b * s_bs + (a_ * oN + c) * s_es] = acc0[i] + acc1[i];
         }
     }
     __syncthreads();
@@ -759,25 +764,28 @@ __device__ __forceinline__ void family_cols_modlp(float2* U, int nb, int bs, int
 // maps, else one wave per map with lanes strided over its values and shuffle sums (a map of the
 // reference's 128^2 J=2 geometry holds 1024 values: 11.4 -> 3.2 ms per 256 RGB patches).
 // Called by every thread of the block (whole waves).
+// S addressing as lds_lowpass_mfma (s_bs < 0: contiguous maps).
 __device__ __forceinline__ void emit(const float* S, int nb, int k0, long long img, int K, int oM,
-                                     int oN, float* out, int pooled) {
+                                     int oN, float* out, int pooled, int s_bs = -1, int s_es = 1) {
     const int npix = oM * oN;
+    if (s_bs < 0) s_bs = npix;
     if (!pooled) {
         const int tot = nb * npix;
         const wstfft::FastDiv dpix(npix);
         for (int o = threadIdx.x; o < tot; o += blockDim.x) {
             const int b = dpix.div(o);
-            out[(img * K + k0 + b) * npix + (o - b * npix)] = S[o];
+            const int i = o - b * npix;
+            out[(img * K + k0 + b) * npix + i] = S[b * s_bs + i * s_es];
         }
     } else if (npix <= 32) {   // small maps (the headline's 4 x 4): one thread per map
         for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-            const float* v = S + b * npix;
+            const float* v = S + b * s_bs;
             float m = 0.f;
-            for (int i = 0; i < npix; ++i) m += v[i];
+            for (int i = 0; i < npix; ++i) m += v[i * s_es];
             m /= npix;
             float q = 0.f;
             for (int i = 0; i < npix; ++i) {
-                const float d = v[i] - m;
+                const float d = v[i * s_es] - m;
                 q = fmaf(d, d, q);
             }
             out[img * 2 * K + k0 + b] = m;
@@ -786,13 +794,13 @@ __device__ __forceinline__ void emit(const float* S, int nb, int k0, long long i
     } else {
         const int lane = threadIdx.x & 63, nw = (blockDim.x + 63) >> 6;
         for (int b = threadIdx.x >> 6; b < nb; b += nw) {
-            const float* v = S + b * npix;
+            const float* v = S + b * s_bs;
             float m = 0.f;
-            for (int i = lane; i < npix; i += 64) m += v[i];
+            for (int i = lane; i < npix; i += 64) m += v[i * s_es];
             m = group_sum<64>(m) / npix;
             float q = 0.f;
             for (int i = lane; i < npix; i += 64) {
-                const float d = v[i] - m;
+                const float d = v[i * s_es] - m;
                 q = fmaf(d, d, q);
             }
             q = group_sum<64>(q);
@@ -1292,6 +1300,42 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     // 5. split into the two rows' half spectra (columns 0..nN1/2) and export them
     const int hld = (nN1 >> 1) + 1;
     float2* H = hexp + static_cast<long long>(item) * nM1 * hld;
+    if (lay.export_full) {
+        // in place: packed row 2t -> half-spectrum rows 2t and 2t+1 (the odd rows of A are free),
+        // then the column FFTs (rows digit-reversed -> natural); k_o2 folds the fully transformed
+        // spectrum from HBM/L2 and keeps only its path batches in LDS (host: nh * hld <= KS * T)
+        constexpr int KS = 8;
+        const int T = blockDim.x, nitems = nh * hld;
+        const wstfft::FastDiv dh(hld);
+        float2 e0[KS], e1[KS];
+        int dst[KS];
+#pragma unroll
+        for (int k = 0; k < KS; ++k) {
+            const int w = threadIdx.x + k * T;
+            dst[k] = -1;
+            if (w < nitems) {
+                const int t = dh.div(w), v = w - t * hld;
+                const float2* row = A + (2 * t) * ld1;
+                const float2 z = row[v];
+                const float2 zm = row[v == 0 ? 0 : nN1 - v];
+                e0[k] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+                e1[k] = make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
+                dst[k] = (2 * t) * ld1 + v;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < KS; ++k)
+            if (dst[k] >= 0) {
+                A[dst[k]] = e0[k];
+                A[dst[k] + ld1] = e1[k];
+            }
+        __syncthreads();
+        lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(A, wstfft::Lines{1, 0, hld, 1, ld1}, nM1,
+                                                                     tb.twM(j1), id);
+        for (GridIter it(hld); it.u < nM1; it.next()) stnt(H + it.u * hld + it.v, A[it.u * ld1 + it.v]);
+        return;
+    }
     for (GridIter it(hld); it.u < nh; it.next()) {
         const float2* row = A + (2 * it.u) * ld1;
         const float2 z = row[it.v];
@@ -1415,13 +1459,20 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                     lds_fft2<FM, FN, 0, MAXN, kDR, true>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
                                                          tb.twN(j2), mod2);
                 if (!(dbg & 64)) {
-                    if (wide_lowpass(p))
+                    const int k0 = kbase + (j2 - j1 - 1) * L + l2a;
+                    if (wide_lowpass(p)) {
+                        // the maps go to the .x slots of the arrays (no S region: the exported-
+                        // spectrum k_o2 fits two workgroups per CU); the next fold rewrites B
+                        float* SB = reinterpret_cast<float*>(B);
                         lds_lowpass_mfma(B, npath, pslot, nM2, nN2, ld2, lpw_M(p, j2), lpw_N(p, j2),
-                                         p.oMp, p.oNp, oM, oN, S);
-                    else
+                                         p.oMp, p.oNp, oM, oN, SB, 2 * pslot, 2);
+                        emit(SB, npath, k0, img, p.K, oM, oN, out, pooled, 2 * pslot, 2);
+                        __syncthreads();
+                    } else {
                         lds_lowpass(B, npath, pslot, nM2, nN2, ld2, tb.lpM(j2), tb.lpN(j2), tb.pmM(j2),
-                                tb.pmN(j2), 1 << (J - j2), oM, oN, S);
-                    emit(S, npath, kbase + (j2 - j1 - 1) * L + l2a, img, p.K, oM, oN, out, pooled);
+                                    tb.pmN(j2), 1 << (J - j2), oM, oN, S);
+                        emit(S, npath, k0, img, p.K, oM, oN, out, pooled);
+                    }
                 }
             }
             // no barrier here: the next batch's fold writes B only, and S is rewritten only after

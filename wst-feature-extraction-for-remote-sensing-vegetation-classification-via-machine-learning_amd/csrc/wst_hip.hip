@@ -173,6 +173,10 @@ struct wst_plan {
     float* d_lpn = nullptr;
     float* d_lpw = nullptr;                       // wide tap matrices (MFMA low-pass)
     int* d_lpw_off = nullptr;
+    std::vector<int> o2_export;                   // per resident j1: k_o1 exports the full spectrum,
+    std::vector<LdsLayout> o2x_lay;               //   k_o2 folds it from HBM (HG = 1, no spectrum in
+    std::vector<size_t> o2x_lds;                  //   LDS): two workgroups per CU where the spectrum
+    std::vector<int> o2x_threads;                 //   held them to one
     std::vector<LdsLayout> hg_lay;                // k_o2 (global spectrum) after a staged j1
     std::vector<size_t> hg_lds;
     std::vector<int> hg_threads, hg_j2first;
@@ -809,6 +813,37 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                          plan->cap[j1], plan->o1_threads[j1], plan->o1_lds[j1], plan->o2_threads[j1],
                          plan->o2_lds[j1]);
     }
+    // Wide-output square levels whose k_o2 holds one workgroup per CU because of the level-j1
+    // spectrum in LDS (the reference's 128^2 J=2 geometry: 75 KB spectrum + 75 KB path batch): k_o1
+    // exports the fully transformed spectrum and k_o2 folds it from HBM / L2, two workgroups per CU.
+    plan->o2_export.assign(J, 0);
+    plan->o2x_lay.assign(J, LdsLayout{});
+    plan->o2x_lds.assign(J, 0);
+    plan->o2x_threads.assign(J, 64);
+    bool export_on = true;
+    if (const char* e = diag_env("WST_O2_EXPORT")) export_on = std::atoi(e) != 0;
+    for (int j1 = plan->rb; j1 + 1 < J && max_order >= 2; ++j1) {
+        const int nM1 = g.PM >> j1, nN1 = g.PN >> j1, hld = nN1 / 2 + 1;
+        if (!export_on || plan->sq || g.PM != g.PN || plan->fam_m == 0 || plan->fam_m != plan->fam_n ||
+            plan->cap[j1] != 136 || plan->o2_lds[j1] <= static_cast<size_t>(kMaxLds) / 2)
+            continue;
+        size_t bcap = 2 * pslot(j1 + 1);
+        if (j1 + 2 < J) bcap = std::max(bcap, static_cast<size_t>(L) * pslot(j1 + 2));
+        size_t smax = 0;
+        for (int j2 = j1 + 1; j2 < J; ++j2)
+            smax = std::max(smax, static_cast<size_t>(paths_per_batch(bcap, pslot(j2), L)) * omn);
+        // wide maps are written into the path arrays themselves (no S region); square: M-side
+        // twiddle tables serve both dimensions
+        const size_t lds = layout(plan->o2x_lay[j1], 0, bcap * sizeof(float2), t, Blocks{j1, J - 1, false},
+                                  j1 + 1, J - 1, (g.oM > wstdev::kLpOM || g.oN > wstdev::kLpOM) ? 0 : smax);
+        if (lds > static_cast<size_t>(kMaxLds) / 2) continue;
+        const int o1t = fill_cu(plan->o1_threads[j1], plan->o1_lds[j1]);
+        if ((nM1 / 2) * hld > 8 * o1t) continue;   // k_o1's in-place split holds 8 items per thread
+        plan->o2_export[j1] = 1;
+        plan->o2x_lds[j1] = lds;
+        plan->o2x_threads[j1] = fill_cu(default_threads(static_cast<size_t>(nM1) * nN1), lds, 768);
+        plan->o1_lay[j1].export_full = 1;
+    }
     for (int j1 = plan->rb; j1 < J; ++j1) {
         plan->o1_threads[j1] = fill_cu(plan->o1_threads[j1], plan->o1_lds[j1]);
         if (plan->o2_lds[j1] > 0) plan->o2_threads[j1] = fill_cu(plan->o2_threads[j1], plan->o2_lds[j1], 768);
@@ -816,6 +851,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     if (plan->rb == 0) plan->prep_threads = fill_cu(static_cast<int>(plan->prep_threads), plan->prep_lds);
     threads_override("WST_O1_THREADS", plan->o1_threads);
     threads_override("WST_O2_THREADS", plan->o2_threads);
+    threads_override("WST_O2X_THREADS", plan->o2x_threads);
     WST_HIP_CHECK(plan->ops->set_attrs());
     if (plan->rb > 0) {
         WST_HIP_CHECK(wstlaunch::wst_big_common_ops().set_attrs());
@@ -914,6 +950,12 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
     if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
     if (!do2) return WST_OK;
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
+    if (plan->o2_export[j1]) {   // spectrum exported fully transformed: fold from HBM
+        plan->ops->o2(136, 0, 1, Launch{dim3(nimg * g.L), dim3(plan->o2x_threads[j1]), plan->o2x_lds[j1], stream},
+                      plan->dp, plan->o2x_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j1 + 1);
+        WST_HIP_CHECK(hipGetLastError());
+        return timer.end(stream, 1 + g.J + j1);
+    }
     plan->ops->o2(plan->cap[j1], plan->sq, 0,
                   Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
                   plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j1 + 1);

@@ -39,6 +39,9 @@ hipError_t set_attrs() {
     if ((e = attrs_all<0>()) != hipSuccess) return e;
     if constexpr (kSquareFamily) {
         if ((e = attrs_all<1>()) != hipSuccess) return e;
+        if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2<FM, FN, 136, 0, 1>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds)) != hipSuccess)
+            return e;
         return hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2<FM, FN, 136, 1, 1>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds);
     }
@@ -91,7 +94,10 @@ void o1(int cap, int sq, const Launch& q, const DevParams& dp, const LdsLayout& 
 void o2(int cap, int sq, int hg, const Launch& q, const DevParams& dp, const LdsLayout& lay, int j1,
         int nimg, long long img0, const float2* hexp, float* out, int pooled, int j2first) {
     if constexpr (kSquareFamily) {
-        if (hg) return o2_sq<1, 1>(cap, q, dp, lay, j1, nimg, img0, hexp, out, pooled, j2first);
+        // hg: the spectrum in HBM -- after a staged big level (square fused kernels) or exported
+        // fully transformed by k_o1 for a wide-output level (plan o2_export)
+        if (hg) return sq ? o2_sq<1, 1>(cap, q, dp, lay, j1, nimg, img0, hexp, out, pooled, j2first)
+                          : o2_sq<0, 1>(cap, q, dp, lay, j1, nimg, img0, hexp, out, pooled, j2first);
         if (sq) return o2_sq<1, 0>(cap, q, dp, lay, j1, nimg, img0, hexp, out, pooled, j2first);
     }
     o2_sq<0, 0>(cap, q, dp, lay, j1, nimg, img0, hexp, out, pooled, j2first);
