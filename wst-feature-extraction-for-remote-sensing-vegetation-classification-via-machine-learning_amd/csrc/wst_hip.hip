@@ -825,7 +825,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     for (int j1 = plan->rb; j1 + 1 < J && max_order >= 2; ++j1) {
         const int nM1 = g.PM >> j1, nN1 = g.PN >> j1, hld = nN1 / 2 + 1;
         if (!export_on || plan->sq || g.PM != g.PN || plan->fam_m == 0 || plan->fam_m != plan->fam_n ||
-            plan->cap[j1] != 136 || plan->o2_lds[j1] <= static_cast<size_t>(kMaxLds) / 2)
+            plan->cap[j1] != 136)
             continue;
         size_t bcap = 2 * pslot(j1 + 1);
         if (j1 + 2 < J) bcap = std::max(bcap, static_cast<size_t>(L) * pslot(j1 + 2));
@@ -836,7 +836,8 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         // twiddle tables serve both dimensions
         const size_t lds = layout(plan->o2x_lay[j1], 0, bcap * sizeof(float2), t, Blocks{j1, J - 1, false},
                                   j1 + 1, J - 1, (g.oM > wstdev::kLpOM || g.oN > wstdev::kLpOM) ? 0 : smax);
-        if (lds > static_cast<size_t>(kMaxLds) / 2) continue;
+        // worth it when the freed spectrum lets more workgroups share a CU
+        if (kMaxLds / lds <= kMaxLds / plan->o2_lds[j1]) continue;
         const int o1t = fill_cu(plan->o1_threads[j1], plan->o1_lds[j1]);
         if ((nM1 / 2) * hld > 8 * o1t) continue;   // k_o1's in-place split holds 8 items per thread
         plan->o2_export[j1] = 1;
