@@ -1072,6 +1072,8 @@ __device__ __forceinline__ void fold2(const float2* __restrict__ H, int hld, int
 // Each lane keeps one column v (its mirror column and sign are fixed) and walks the rows
 // (pair, u) of the batch in steps of rpp = T / nN2 (lanes beyond rpp * nN2 idle); the filter
 // taps come through a buffer descriptor with the row offsets as wave-uniform soffsets.
+// R rows of a lane in flight per iteration (R = 2 when H is read from HBM / L2: HG kernels).
+template <int R = 1>
 __device__ __forceinline__ void fold2_s2(const float2* __restrict__ H, int hld, int nM1, int nN1,
                                          const float2* __restrict__ psi2, long long pstride,
                                          int npair, int npath, float2* __restrict__ B, int pslot,
@@ -1088,41 +1090,52 @@ __device__ __forceinline__ void fold2_s2(const float2* __restrict__ H, int hld, 
     const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, static_cast<int>(npair * pstride * 8));
     const wstfft::FastDiv dm(nM2);
     const int rows = npair * nM2;
-    for (int pu = t0; pu < rows; pu += rpp) {
-        const int pr = dm.div(pu);
-        const int u = pu - pr * nM2;
-        const int hr = u * hld;
-        const int hm0 = v0 ? hr : (u == 0 ? 0 : (nM1 - u) * hld);
-        const int hm1 = v0 ? hr + hq : (nM2 - u) * hld;
-        float2 h[4];
-        h[0] = H[hr + v];
-        h[1] = H[hm0 + cB];
-        h[2] = H[hr + hq + v];
-        h[3] = H[hm1 + cB];
-        h[1].y *= sg;
-        h[3].y *= sg;
-        const int fo = (static_cast<int>(pr * pstride) + u * nN1 + v) * 8;
-        float2 f[4];
-        f[0] = buf_load2(rs, fo, 0);
-        f[1] = buf_load2(rs, fo, nN2 * 8);
-        f[2] = buf_load2(rs, fo, fq);
-        f[3] = buf_load2(rs, fo, fq + nN2 * 8);
-        float2 a0, a1;
-        a0.x = fmaf(h[0].x, f[0].x, fmaf(h[1].x, f[1].x, fmaf(h[2].x, f[2].x, h[3].x * f[3].x)));
-        a0.y = fmaf(h[0].y, f[0].x, fmaf(h[1].y, f[1].x, fmaf(h[2].y, f[2].x, h[3].y * f[3].x)));
-        a1.x = fmaf(h[0].x, f[0].y, fmaf(h[1].x, f[1].y, fmaf(h[2].x, f[2].y, h[3].x * f[3].y)));
-        a1.y = fmaf(h[0].y, f[0].y, fmaf(h[1].y, f[1].y, fmaf(h[2].y, f[2].y, h[3].y * f[3].y)));
-        float2* dst = B + 2 * pr * pslot + u * ld2 + v;
-        dst[0] = a0;
-        if (2 * pr + 1 < npath) dst[pslot] = a1;
+    for (int pu0 = t0; pu0 < rows; pu0 += R * rpp) {
+        float2 h[R][4], f[R][4];
+        int pr[R], dst[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int pu = min(pu0 + r * rpp, rows - 1);
+            pr[r] = dm.div(pu);
+            const int u = pu - pr[r] * nM2;
+            dst[r] = pu0 + r * rpp < rows ? 2 * pr[r] * pslot + u * ld2 + v : -1;
+            const int hr = u * hld;
+            const int hm0 = v0 ? hr : (u == 0 ? 0 : (nM1 - u) * hld);
+            const int hm1 = v0 ? hr + hq : (nM2 - u) * hld;
+            h[r][0] = H[hr + v];
+            h[r][1] = H[hm0 + cB];
+            h[r][2] = H[hr + hq + v];
+            h[r][3] = H[hm1 + cB];
+            const int fo = (static_cast<int>(pr[r] * pstride) + u * nN1 + v) * 8;
+            f[r][0] = buf_load2(rs, fo, 0);
+            f[r][1] = buf_load2(rs, fo, nN2 * 8);
+            f[r][2] = buf_load2(rs, fo, fq);
+            f[r][3] = buf_load2(rs, fo, fq + nN2 * 8);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            h[r][1].y *= sg;
+            h[r][3].y *= sg;
+            float2 a0, a1;
+            a0.x = fmaf(h[r][0].x, f[r][0].x, fmaf(h[r][1].x, f[r][1].x, fmaf(h[r][2].x, f[r][2].x, h[r][3].x * f[r][3].x)));
+            a0.y = fmaf(h[r][0].y, f[r][0].x, fmaf(h[r][1].y, f[r][1].x, fmaf(h[r][2].y, f[r][2].x, h[r][3].y * f[r][3].x)));
+            a1.x = fmaf(h[r][0].x, f[r][0].y, fmaf(h[r][1].x, f[r][1].y, fmaf(h[r][2].x, f[r][2].y, h[r][3].x * f[r][3].y)));
+            a1.y = fmaf(h[r][0].y, f[r][0].y, fmaf(h[r][1].y, f[r][1].y, fmaf(h[r][2].y, f[r][2].y, h[r][3].y * f[r][3].y)));
+            if (dst[r] >= 0) {
+                float2* d = B + dst[r];
+                d[0] = a0;
+                if (2 * pr[r] + 1 < npath) d[pslot] = a1;
+            }
+        }
     }
 }
 
+template <int R = 1>
 __device__ __forceinline__ void fold2_any(int s2, const float2* H, int hld, int nM1, int nN1,
                                           const float2* psi2, long long pstride, int npair,
                                           int npath, float2* B, int pslot, int ld2, int nM2,
                                           int nN2, const int* box, int bstride) {
-    if (s2 == 2) fold2_s2(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
+    if (s2 == 2) fold2_s2<R>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
     else fold2<0>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, s2, box, bstride);
 }
 
@@ -1434,7 +1447,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             const long long pstride = static_cast<long long>(n1);
             const int* bx = p.box + p.box_off[j2 * J + j1] + (l2a >> 1) * (nM2 + nN2);
             if (!(dbg & 8))
-                fold2_any(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
+                fold2_any<HG ? 2 : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
                           bx, nM2 + nN2);
             __syncthreads();
             WST_STAMP(sctr);
