@@ -181,6 +181,8 @@ struct wst_plan {
     std::vector<size_t> hg_lds;
     std::vector<int> hg_threads, hg_j2first;
     std::vector<size_t> big_rows_lds, big_cols_lds;   // per staged level (2 R lines / 16 columns)
+    std::vector<int> fold_all_rows;               // per staged level: rows of the all-paths s = 2
+    std::vector<size_t> fold_all_lds;             //   order-2 row pass (0: per-pair passes)
     std::vector<size_t> ws_hbig;                  // U1hat half spectra of staged j1 (per plane)
     size_t ws_tmp = 0, ws_ureal = 0, ws_part = 0, ws_csum = 0, ws_mean = 0;
     int64_t max_chunk = 2048;                     // planes per workspace chunk
@@ -687,6 +689,20 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                                                      std::to_string(g.PM >> r));
         plan->big_rows_lds.assign(plan->rb, 0);
         plan->big_cols_lds.assign(plan->rb, 0);
+        // the all-paths s = 2 order-2 row pass: 4 rows x L paths of lines, two workgroups per CU
+        plan->fold_all_rows.assign(plan->rb, 0);
+        plan->fold_all_lds.assign(plan->rb, 0);
+        for (int r = 1; r < plan->rb; ++r) {
+            const size_t n = static_cast<size_t>(g.PM >> r);
+            for (int rows = 4; rows >= 1; rows /= 2) {
+                const size_t lds = (n + static_cast<size_t>(L) * rows * (n | 1)) * sizeof(float2);
+                if (n % rows == 0 && lds <= static_cast<size_t>(kMaxLds) / 2) {
+                    plan->fold_all_rows[r] = rows;
+                    plan->fold_all_lds[r] = lds;
+                    break;
+                }
+            }
+        }
         for (int r = 0; r < plan->rb; ++r) {
             const size_t n = static_cast<size_t>(g.PM >> r);
             plan->big_rows_lds[r] = (n + 2 * kBigRows * (n | 1)) * sizeof(float2);
@@ -822,6 +838,8 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     plan->o2x_threads.assign(J, 64);
     bool export_on = true;
     if (const char* e = diag_env("WST_O2_EXPORT")) export_on = std::atoi(e) != 0;
+    if (const char* e = diag_env("WST_FOLD_ALL"))
+        if (std::atoi(e) == 0) std::fill(plan->fold_all_rows.begin(), plan->fold_all_rows.end(), 0);
     for (int j1 = plan->rb; j1 + 1 < J && max_order >= 2; ++j1) {
         const int nM1 = g.PM >> j1, nN1 = g.PN >> j1, hld = nN1 / 2 + 1;
         if (!export_on || plan->sq || g.PM != g.PN || plan->fam_m == 0 || plan->fam_m != plan->fam_n ||
@@ -1075,7 +1093,13 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
                 f.npair = nq;
                 f.npath = L;
                 f.dst = tmp;
-                B2->rows(true, Launch{dim3(n2 / f.rows, nimg), tb, plan->big_rows_lds[j2], stream}, dp, f);
+                size_t flds = plan->big_rows_lds[j2];
+                if (n1 == 2 * n2 && plan->fold_all_rows[j2] > 0) {
+                    f.fold_all = 1;
+                    f.rows = plan->fold_all_rows[j2];
+                    flds = plan->fold_all_lds[j2];
+                }
+                B2->rows(true, Launch{dim3(n2 / f.rows, nimg), tb, flds, stream}, dp, f);
                 BigArgs m2 = args(kColModLp, j2);
                 m2.dst = tmp;
                 m2.vpart = part;

@@ -59,6 +59,8 @@ struct BigArgs {
     const int* box;              // alias boxes of the pairs (s >= 4), stride n + n
     int npair, npath;            // pairs / paths per (plane, l1); one launch per l1, one
                                  // workgroup per (plane, row block) loops over the pairs
+    int fold_all;                // kRowFold2, s = 2: every path of the block folded from one
+                                 // read of the spectrum taps, one FFT pass over npath * rows lines
     // outputs
     float2* dst;
     float* uout;                 // kColModLp: U real (optional)
@@ -155,6 +157,47 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
         const int s = n1 / N, smask = s - 1;
         const float2* H = a.hsrc + (static_cast<long long>(arr) * a.L + a.l1) * n1 * hld;
         wstfft::EpiIdentity id;
+        if (a.fold_all) {
+            // s = 2 (dense): the four spectrum taps of an output bin are read once and serve every
+            // pair's filters (the per-pair passes re-read the spectrum from HBM: 8.5x the compulsory
+            // bytes at c5); path p of row rr lands on line p * rows + rr
+            for (int i = threadIdx.x; i < a.rows * N; i += T) {
+                const int rr = i / N, v = i - (i / N) * N;
+                const int u = r0 + rr;
+                float2 h[4];
+                long long fo[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int kr = u + (t >> 1) * N, kc = v + (t & 1) * N;
+                    const int krm = kr == 0 ? 0 : n1 - kr;
+                    const bool mir = kc > half;
+                    h[t] = H[mir ? krm * hld + (n1 - kc) : kr * hld + kc];
+                    h[t].y = mir ? -h[t].y : h[t].y;
+                    fo[t] = static_cast<long long>(kr) * n1 + kc;
+                }
+                for (int pr = 0; pr < a.npair; ++pr) {
+                    const float2* ps = a.psi2 + pr * a.pstride;
+                    float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const float2 f = ps[fo[t]];
+                        a0 = make_float2(fmaf(h[t].x, f.x, a0.x), fmaf(h[t].y, f.x, a0.y));
+                        a1 = make_float2(fmaf(h[t].x, f.y, a1.x), fmaf(h[t].y, f.y, a1.y));
+                    }
+                    A[(2 * pr * a.rows + rr) * ld + v] = a0;
+                    if (2 * pr + 1 < a.npath) A[((2 * pr + 1) * a.rows + rr) * ld + v] = a1;
+                }
+            }
+            __syncthreads();
+            wstfft::fft_lines<N, INV>(A, wstfft::Lines(1, 0, a.npath * a.rows, ld, 1), tw, id);
+            for (int i = threadIdx.x; i < a.npath * a.rows * N; i += T) {
+                const int line = i / N, q = i - (i / N) * N;
+                const int path = line / a.rows, rr = line - path * a.rows;
+                float2* D = a.dst + (static_cast<long long>(arr) * a.npath + path) * N * N;
+                wstdev::stnt(D + (r0 + rr) * N + q, A[line * ld + q]);
+            }
+            return;
+        }
         for (int pr = 0; pr < a.npair; ++pr) {
             const float2* ps = a.psi2 + pr * a.pstride;
             const int* bx = a.box + pr * (N + N);
