@@ -759,8 +759,10 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
             smax = std::max(smax, static_cast<size_t>(paths_per_batch(bcap, pslot(j2), L)) * omn);
         plan->hg_lds[j1] = layout(plan->hg_lay[j1], 0, bcap * sizeof(float2), t, Blocks{j2f, J - 1, false},
                                   1, 0, smax, Blocks{j2f, J - 1, false}, oms);
+        // (one workgroup per CU at c5's 96^2 batches: 1024 threads, k_o2 j1=0/1 17.9/3.19 -> 16.7/2.84 ms)
         plan->hg_threads[j1] = default_threads(static_cast<size_t>(g.PM >> j2f) * (g.PN >> j2f));
         if (plan->hg_lds[j1] > static_cast<size_t>(kMaxLds)) return too_big("k_o2 (global spectrum)", j1);
+        plan->hg_threads[j1] = fill_cu(plan->hg_threads[j1], plan->hg_lds[j1]);
     }
     if (plan->rb > 0) {
         plan->ws_tmp = wsp;
@@ -871,6 +873,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     threads_override("WST_O1_THREADS", plan->o1_threads);
     threads_override("WST_O2_THREADS", plan->o2_threads);
     threads_override("WST_O2X_THREADS", plan->o2x_threads);
+    threads_override("WST_HG_THREADS", plan->hg_threads);
     WST_HIP_CHECK(plan->ops->set_attrs());
     if (plan->rb > 0) {
         WST_HIP_CHECK(wstlaunch::wst_big_common_ops().set_attrs());
