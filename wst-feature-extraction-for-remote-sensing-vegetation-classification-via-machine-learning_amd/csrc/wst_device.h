@@ -647,6 +647,10 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
     constexpr bool single = (F::N2 == 1);
     constexpr int RU = single ? NN : F::N2;  // rows per unit
     constexpr int NU = single ? 1 : F::N1;   // units per column
+    // grouped: the NU units of a column sit in NU adjacent lanes and their partials are summed
+    // there (DPP), so the S pass reads one partial per column instead of NU
+    constexpr bool grouped = !single && (NU & (NU - 1)) == 0 && NU <= 16;
+    constexpr int NUS = grouped ? 1 : NU;    // partials per column left for the S pass
     const wstfft::Lines g(nb, bs, cols, 1, ld);
     const int T = blockDim.x;
     const int nlines = nb * cols;
@@ -656,7 +660,10 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
     }
     for (int u = threadIdx.x; u < nlines * NU; u += T) {
         int k = 0;
-        const int line = single ? u : g.split(u, k);
+        int line;
+        if constexpr (single) line = u;
+        else if constexpr (grouped) { line = u / NU; k = u & (NU - 1); }
+        else line = g.split(u, k);
         float2* p = U + g.offset(line) + (RU * k) * ld;
         float2 v[RU];
         wstfft::static_for<0, RU>([&](auto ec) {
@@ -705,6 +712,12 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
                 V[7] = fmaf(g1.w, m, V[7]);
             }
         });
+        if constexpr (grouped) {
+#pragma unroll
+            for (int a = 0; a < kLpOM; ++a)
+                if (a < oM) V[a] = group_sum<NU>(V[a]);
+            if (k != 0) continue;
+        }
 #pragma unroll
         for (int t = 0; t < kLpOM / 2; ++t)
             if (2 * t < oM) p[t * ld] = make_float2(V[2 * t], V[2 * t + 1]);
@@ -727,7 +740,7 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
         float acc = 0.f;
         for (int q = qc; q < cols; q += QC) {
             float wq = 0.f;
-            wstfft::static_for<0, NU>([&](auto kc) {
+            wstfft::static_for<0, NUS>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 wq += f[2 * (q + RU * k * ld)];
             });
