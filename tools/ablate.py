@@ -6,7 +6,11 @@ and runs it through WST_LIB=libwst_hip_diag.so."""
 import os, subprocess, sys, json
 masks = {"full": 0, "no_o1_fold": 128, "no_o1_ifft": 1, "no_S1": 2, "no_U1_fft": 4, "no_o2_fold": 8,
          "no_o2_ifft": 16, "no_o2_lowpass": 64, "no_order2_paths": 8 | 16 | 64,
-         "o2_only_load": 4 | 8 | 16 | 64}
+         "o2_only_load": 4 | 8 | 16 | 64, "no_o2_fold_s2": 256, "no_o2_fold_box": 512,
+         "no_o2_spectrum_load": 1024}
+LIB = os.environ.get("ABL_LIB", "libwst_hip_diag.so")
+if len(sys.argv) > 1:
+    masks = {k: v for k, v in masks.items() if k in sys.argv[1:]}
 child = r'''
 import os, sys, json
 sys.path.insert(0, os.getcwd())
@@ -27,7 +31,7 @@ print(json.dumps([a/3 for a in acc]))
 '''
 res = {}
 for name, m in masks.items():
-    env = dict(os.environ, WST_DEBUG_SKIP=str(m), WST_LIB="libwst_hip_diag.so")
+    env = dict(os.environ, WST_DEBUG_SKIP=str(m), WST_LIB=LIB)
     r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=300)
     line = [l for l in r.stdout.splitlines() if l.startswith("[")]
     res[name] = json.loads(line[-1]) if line else r.stderr[-300:]

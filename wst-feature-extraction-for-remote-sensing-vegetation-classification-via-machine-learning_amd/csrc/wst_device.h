@@ -106,6 +106,8 @@ struct LdsLayout {
     int bcap;               // complex capacity of B (k_o2)
     int export_full;        // k_o1: export the fully transformed half spectra (natural order) for a
                             // k_o2 that folds from HBM (HG = 1) instead of the row-transformed ones
+    int nsplit;             // k_o2 HG: workgroups per (plane, theta1), batch b run by workgroup
+                            // b % nsplit; one item's workgroups share an XCD (its L2 holds H)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -1143,11 +1145,77 @@ __device__ __forceinline__ void fold2_s2(const float2* __restrict__ H, int hld, 
     }
 }
 
+// s = 2 fold, PU pairs of the batch from one read of the four spectrum taps: the lane of column
+// v walks the (pair group, row u) items, reads H's taps once per item and folds its PU pairs
+// (PU x 4 filter loads in flight), so the batch reads the spectrum npair / PU times, not npair.
+template <int PU = 2>
+__device__ __forceinline__ void fold2_s2_pairs(const float2* __restrict__ H, int hld, int nM1, int nN1,
+                                               const float2* __restrict__ psi2, long long pstride,
+                                               int npair, int npath, float2* __restrict__ B, int pslot,
+                                               int ld2, int nM2, int nN2) {
+    const int rpp = blockDim.x / nN2;
+    const int t0 = threadIdx.x / nN2;
+    if (t0 >= rpp) return;
+    const int v = threadIdx.x - t0 * nN2;
+    const bool v0 = v == 0;
+    const int cB = v0 ? nN2 : nN2 - v;
+    const float sg = v0 ? 1.f : -1.f;
+    const int hq = nM2 * hld;
+    const int fq = nM2 * nN1 * 8;
+    const int ps8 = static_cast<int>(pstride * 8);
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, static_cast<int>(npair * pstride * 8));
+    const int ngrp = (npair + PU - 1) / PU;
+    const wstfft::FastDiv dm(nM2);
+    for (int gu = t0; gu < ngrp * nM2; gu += rpp) {
+        const int g = dm.div(gu);
+        const int u = gu - g * nM2;
+        const int pr0 = g * PU;
+        const int hr = u * hld;
+        const int hm0 = v0 ? hr : (u == 0 ? 0 : (nM1 - u) * hld);
+        const int hm1 = v0 ? hr + hq : (nM2 - u) * hld;
+        float2 h0 = H[hr + v], h1 = H[hm0 + cB], h2 = H[hr + hq + v], h3 = H[hm1 + cB];
+        h1.y *= sg;
+        h3.y *= sg;
+        const int fo = (u * nN1 + v) * 8;
+        float2* d0 = B + u * ld2 + v;
+        {
+            float2 f[PU][4];
+#pragma unroll
+            for (int r = 0; r < PU; ++r) {
+                const int so = min(pr0 + r, npair - 1) * ps8;
+                f[r][0] = buf_load2(rs, fo, so);
+                f[r][1] = buf_load2(rs, fo, so + nN2 * 8);
+                f[r][2] = buf_load2(rs, fo, so + fq);
+                f[r][3] = buf_load2(rs, fo, so + fq + nN2 * 8);
+            }
+#pragma unroll
+            for (int r = 0; r < PU; ++r) {
+                const int pr = pr0 + r;
+                if (pr >= npair) break;
+                float2 a0, a1;
+                a0.x = fmaf(h0.x, f[r][0].x, fmaf(h1.x, f[r][1].x, fmaf(h2.x, f[r][2].x, h3.x * f[r][3].x)));
+                a0.y = fmaf(h0.y, f[r][0].x, fmaf(h1.y, f[r][1].x, fmaf(h2.y, f[r][2].x, h3.y * f[r][3].x)));
+                a1.x = fmaf(h0.x, f[r][0].y, fmaf(h1.x, f[r][1].y, fmaf(h2.x, f[r][2].y, h3.x * f[r][3].y)));
+                a1.y = fmaf(h0.y, f[r][0].y, fmaf(h1.y, f[r][1].y, fmaf(h2.y, f[r][2].y, h3.y * f[r][3].y)));
+                float2* d = d0 + 2 * pr * pslot;
+                d[0] = a0;
+                if (2 * pr + 1 < npath) d[pslot] = a1;
+            }
+        }
+    }
+}
+
 template <int R = 1>
 __device__ __forceinline__ void fold2_any(int s2, const float2* H, int hld, int nM1, int nN1,
                                           const float2* psi2, long long pstride, int npair,
                                           int npath, float2* B, int pslot, int ld2, int nM2,
                                           int nN2, const int* box, int bstride) {
+#ifdef WST_FOLD_PAIRS
+    if (s2 == 2 && R == 1) {
+        fold2_s2_pairs<WST_FOLD_PAIRS>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
+        return;
+    }
+#endif
     if (s2 == 2) fold2_s2<R>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
     else fold2<0>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, s2, box, bstride);
 }
@@ -1409,7 +1477,25 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     const int oM = OC ? OC : p.oM, oN = OC ? OC : p.oN;
     const int oms = OC ? 4 : lay.oms;
     const int J = p.J, L = p.L;
-    const int item = xcd_item(nimg * L);
+    const int nsplit = HG ? max(1, lay.nsplit) : 1;
+    int item, ksplit = 0;
+    if (nsplit > 1) {
+        // blocks x and x + 8 share an XCD: the nsplit workgroups of an item take consecutive
+        // dispatch slots of one XCD, so they run together and read H through the same L2
+        const int total = nimg * L;
+        const int x = blockIdx.x;
+        if ((total & 7) == 0) {
+            const int slot = x >> 3;
+            const int il = slot / nsplit;
+            ksplit = slot - il * nsplit;
+            item = (x & 7) * (total >> 3) + il;
+        } else {
+            item = x / nsplit;
+            ksplit = x - item * nsplit;
+        }
+    } else {
+        item = xcd_item(nimg * L);
+    }
     const int local = item / L;
     const int l1 = item - local * L;
     const long long img = img0 + local;
@@ -1435,7 +1521,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     if constexpr (!HG) {
         // 1. half spectrum rows -> LDS, then the column FFTs (rows digit-reversed -> natural)
         float2* Hl = reinterpret_cast<float2*>(smem);
-        copy_to_lds(Hl, Hg, nM1 * hld);
+        if (!(dbg & 1024)) copy_to_lds(Hl, Hg, nM1 * hld);
         __syncthreads();
         if (!(dbg & 4))
             lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(
@@ -1446,6 +1532,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     // 2. order-2 paths in batches: Hermitian fold -> |ifft| -> S2 low-pass
     const int kbase = p.o2_base[j1 * L + l1];
     const int nq = (L + 1) >> 1;
+    int bctr = 0;   // batch counter (split HG launches)
     // every batch of paths of level j2 (sizes nM2 x nN2)
     auto level = [&](int j2, int nM2, int nN2) __attribute__((always_inline)) {
         const int ld2 = odd_ld(nN2);
@@ -1454,12 +1541,16 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
         int pb = lay.bcap / pslot;                 // paths per batch (multiple of 2)
         pb = max(2, min(pb & ~1, 2 * nq));
         for (int l2a = 0; l2a < L; l2a += pb) {
+            if (nsplit > 1) {
+                const int bi = bctr++;
+                if (bi % nsplit != ksplit) continue;
+            }
             const int npath = min(pb, L - l2a);
             const int npair = (npath + 1) >> 1;
             const float2* ps = p.psi2 + p.psi2_off[(j2 * J + j1) * nq + (l2a >> 1)];
             const long long pstride = static_cast<long long>(n1);
             const int* bx = p.box + p.box_off[j2 * J + j1] + (l2a >> 1) * (nM2 + nN2);
-            if (!(dbg & 8))
+            if (!(dbg & 8) && !(dbg & (s2 == 2 ? 256 : 512)))
                 fold2_any<HG ? 2 : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
                           bx, nM2 + nN2);
             __syncthreads();

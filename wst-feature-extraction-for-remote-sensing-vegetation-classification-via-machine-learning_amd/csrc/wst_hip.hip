@@ -763,6 +763,15 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         plan->hg_threads[j1] = default_threads(static_cast<size_t>(g.PM >> j2f) * (g.PN >> j2f));
         if (plan->hg_lds[j1] > static_cast<size_t>(kMaxLds)) return too_big("k_o2 (global spectrum)", j1);
         plan->hg_threads[j1] = fill_cu(plan->hg_threads[j1], plan->hg_lds[j1]);
+        // one workgroup per batch: the batches of an item fold from the same H, which one XCD's
+        // L2 then serves (one workgroup per item re-read it from HBM once per batch)
+        int nbatch = 0;
+        for (int j2 = j2f; j2 < J; ++j2) {
+            const int pb = paths_per_batch(bcap, pslot(j2), L);
+            nbatch += (L + pb - 1) / pb;
+        }
+        plan->hg_lay[j1].nsplit = nbatch;
+        if (const char* e = diag_env("WST_HG_SPLIT")) plan->hg_lay[j1].nsplit = std::max(1, std::atoi(e));
     }
     if (plan->rb > 0) {
         plan->ws_tmp = wsp;
@@ -1117,7 +1126,8 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         }
         const int j2f = plan->hg_j2first[j1];
         if (j2f < J)
-            plan->ops->o2(136, 1, 1, Launch{dim3(nimg * L), dim3(plan->hg_threads[j1]), plan->hg_lds[j1], stream},
+            plan->ops->o2(136, 1, 1, Launch{dim3(nimg * L * std::max(1, plan->hg_lay[j1].nsplit)),
+                                            dim3(plan->hg_threads[j1]), plan->hg_lds[j1], stream},
                           dp, plan->hg_lay[j1], j1, nimg, img0, hbig, d_out, pooled, j2f);
         WST_HIP_CHECK(hipGetLastError());
         if ((rc = timer.end(stream, 1 + J + j1)) != WST_OK) return rc;

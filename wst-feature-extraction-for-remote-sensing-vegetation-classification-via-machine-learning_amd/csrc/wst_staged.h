@@ -27,6 +27,7 @@ constexpr int kBigMinN = wstfft::kMaxFamilyN;   // levels with n > kBigMinN are 
 constexpr int kBigThreads = 256;
 constexpr int kColTile = 16;                    // columns per column-pass workgroup (128 B rows)
 constexpr int kMeanParts = 16;                  // k_big_mean partial sums per plane
+constexpr int kLoadBatch = 8;                   // global loads per thread in flight (tile loads)
 
 enum RowMode { kRowPad = 0, kRowReal2 = 1, kRowFold1 = 2, kRowFold2 = 3 };
 enum ColMode { kColStore = 0, kColModLp = 1 };
@@ -127,10 +128,21 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
         nlines = a.rows / 2;
         const float* U = a.ureal + static_cast<long long>(arr) * N * N;
         const float m = a.mean[arr];
-        for (int i = threadIdx.x; i < nlines * N; i += T) {
-            const int t = i / N, q = i - (i / N) * N;
-            const int u = r0 + 2 * t;
-            A[t * ld + q] = make_float2(U[u * N + q] - m, U[(u + 1) * N + q] - m);
+        for (int i0 = threadIdx.x; i0 < nlines * N; i0 += kLoadBatch * T) {
+            float2 t2[kLoadBatch];
+#pragma unroll
+            for (int k = 0; k < kLoadBatch; ++k) {
+                const int i = min(i0 + k * T, nlines * N - 1);
+                const int t = i / N, q = i - (i / N) * N;
+                const int u = r0 + 2 * t;
+                t2[k] = make_float2(U[u * N + q], U[(u + 1) * N + q]);
+            }
+#pragma unroll
+            for (int k = 0; k < kLoadBatch; ++k) {
+                const int i = i0 + k * T;
+                const int t = i / N, q = i - (i / N) * N;
+                if (i < nlines * N) A[t * ld + q] = make_float2(t2[k].x - m, t2[k].y - m);
+            }
         }
     } else if (a.mode == kRowFold1) {
         // arr = plane * L + l1: rows of fold_s(Xhat * psi0_{j1, l1}), Xhat is (N s) x (N s)
@@ -139,6 +151,26 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
         const int PN = N * s;
         const float2* X = a.xhat + static_cast<long long>(plane) * PN * PN;
         const float* psi0 = p.psi + p.psi_off[(a.j1 * a.L + l1) * p.J + 0];
+        if (s == 1) {
+            for (int i0 = threadIdx.x; i0 < a.rows * N; i0 += kLoadBatch * T) {
+                float2 xv[kLoadBatch];
+                float f[kLoadBatch];
+#pragma unroll
+                for (int k = 0; k < kLoadBatch; ++k) {
+                    const int i = min(i0 + k * T, a.rows * N - 1);
+                    const int rr = i / N, q = i - (i / N) * N;
+                    const long long idx = static_cast<long long>(r0 + rr) * PN + q;
+                    f[k] = psi0[idx];
+                    xv[k] = X[idx];
+                }
+#pragma unroll
+                for (int k = 0; k < kLoadBatch; ++k) {
+                    const int i = i0 + k * T;
+                    const int rr = i / N, q = i - (i / N) * N;
+                    if (i < a.rows * N) A[rr * ld + q] = make_float2(xv[k].x * f[k], xv[k].y * f[k]);
+                }
+            }
+        } else
         for (int i = threadIdx.x; i < a.rows * N; i += T) {
             const int rr = i / N, q = i - (i / N) * N;
             const int u = r0 + rr;
@@ -161,31 +193,47 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
             // s = 2 (dense): the four spectrum taps of an output bin are read once and serve every
             // pair's filters (the per-pair passes re-read the spectrum from HBM: 8.5x the compulsory
             // bytes at c5); path p of row rr lands on line p * rows + rr
-            for (int i = threadIdx.x; i < a.rows * N; i += T) {
-                const int rr = i / N, v = i - (i / N) * N;
-                const int u = r0 + rr;
-                float2 h[4];
-                long long fo[4];
+            // KI bins per thread in flight: their 4 KI spectrum taps, then per pair 4 KI filter taps
+            constexpr int KI = 2;
+            for (int i0 = threadIdx.x; i0 < a.rows * N; i0 += KI * T) {
+                float2 h[KI][4];
+                int fo[KI][4];
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int kr = u + (t >> 1) * N, kc = v + (t & 1) * N;
-                    const int krm = kr == 0 ? 0 : n1 - kr;
-                    const bool mir = kc > half;
-                    h[t] = H[mir ? krm * hld + (n1 - kc) : kr * hld + kc];
-                    h[t].y = mir ? -h[t].y : h[t].y;
-                    fo[t] = static_cast<long long>(kr) * n1 + kc;
+                for (int k = 0; k < KI; ++k) {
+                    const int i = min(i0 + k * T, a.rows * N - 1);
+                    const int rr = i / N, v = i - (i / N) * N;
+                    const int u = r0 + rr;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int kr = u + (t >> 1) * N, kc = v + (t & 1) * N;
+                        const int krm = kr == 0 ? 0 : n1 - kr;
+                        const bool mir = kc > half;
+                        h[k][t] = H[mir ? krm * hld + (n1 - kc) : kr * hld + kc];
+                        h[k][t].y = mir ? -h[k][t].y : h[k][t].y;
+                        fo[k][t] = kr * n1 + kc;
+                    }
                 }
                 for (int pr = 0; pr < a.npair; ++pr) {
                     const float2* ps = a.psi2 + pr * a.pstride;
-                    float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+                    float2 f[KI][4];
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const float2 f = ps[fo[t]];
-                        a0 = make_float2(fmaf(h[t].x, f.x, a0.x), fmaf(h[t].y, f.x, a0.y));
-                        a1 = make_float2(fmaf(h[t].x, f.y, a1.x), fmaf(h[t].y, f.y, a1.y));
+                    for (int k = 0; k < KI; ++k)
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) f[k][t] = ps[fo[k][t]];
+#pragma unroll
+                    for (int k = 0; k < KI; ++k) {
+                        const int i = i0 + k * T;
+                        if (i >= a.rows * N) break;
+                        const int rr = i / N, v = i - (i / N) * N;
+                        float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            a0 = make_float2(fmaf(h[k][t].x, f[k][t].x, a0.x), fmaf(h[k][t].y, f[k][t].x, a0.y));
+                            a1 = make_float2(fmaf(h[k][t].x, f[k][t].y, a1.x), fmaf(h[k][t].y, f[k][t].y, a1.y));
+                        }
+                        A[(2 * pr * a.rows + rr) * ld + v] = a0;
+                        if (2 * pr + 1 < a.npath) A[((2 * pr + 1) * a.rows + rr) * ld + v] = a1;
                     }
-                    A[(2 * pr * a.rows + rr) * ld + v] = a0;
-                    if (2 * pr + 1 < a.npath) A[((2 * pr + 1) * a.rows + rr) * ld + v] = a1;
                 }
             }
             __syncthreads();
@@ -282,9 +330,22 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
     const float2* gtw = level_tw(p, a.lvl);
     for (int i = threadIdx.x; i < N; i += T) tw[i] = gtw[i];
     float2* src = a.dst + static_cast<long long>(arr) * N * a.ncols;
-    for (int i = threadIdx.x; i < N * C; i += T) {
-        const int u = i / C, c = i - (i / C) * C;
-        if (c < nc) A[c * ld + u] = wstdev::ldnt(src + static_cast<long long>(u) * a.ncols + c0 + c);
+    // kLoadBatch loads per thread in flight before their LDS stores (a load-store loop waits out
+    // the HBM latency once per element: ~2.2 TB/s at c5)
+    for (int i0 = threadIdx.x; i0 < N * C; i0 += kLoadBatch * T) {
+        float2 t[kLoadBatch];
+#pragma unroll
+        for (int k = 0; k < kLoadBatch; ++k) {
+            const int i = min(i0 + k * T, N * C - 1);
+            const int u = i / C, c = min(i - (i / C) * C, nc - 1);
+            t[k] = wstdev::ldnt(src + static_cast<long long>(u) * a.ncols + c0 + c);
+        }
+#pragma unroll
+        for (int k = 0; k < kLoadBatch; ++k) {
+            const int i = i0 + k * T;
+            const int u = i / C, c = i - (i / C) * C;
+            if (i < N * C && c < nc) A[c * ld + u] = t[k];
+        }
     }
     __syncthreads();
     if (a.mode == kColStore) {
