@@ -303,6 +303,8 @@ size_t layout(LdsLayout& lay, size_t data_a, size_t data_b, const TableOffsets& 
 }
 
 // paths per order-2 batch at level j2 (mirrors k_o2)
+constexpr int kHgSplit = 3;   // k_o2 HG workgroups per (plane, theta1)
+
 int paths_per_batch(size_t bcap, size_t pslot, int L) {
     const int nq = (L + 1) / 2;
     int pb = static_cast<int>(bcap / pslot);
@@ -689,14 +691,15 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                                                      std::to_string(g.PM >> r));
         plan->big_rows_lds.assign(plan->rb, 0);
         plan->big_cols_lds.assign(plan->rb, 0);
-        // the all-paths s = 2 order-2 row pass: 4 rows x L paths of lines, two workgroups per CU
+        // the all-paths s = 2 order-2 row pass: rows x L paths of lines, four workgroups per CU (c5:
+        // 2 rows, 28.96 -> 27.92 ms against 4 rows at two workgroups per CU; 1 row: 28.39)
         plan->fold_all_rows.assign(plan->rb, 0);
         plan->fold_all_lds.assign(plan->rb, 0);
         for (int r = 1; r < plan->rb; ++r) {
             const size_t n = static_cast<size_t>(g.PM >> r);
             for (int rows = 4; rows >= 1; rows /= 2) {
                 const size_t lds = (n + static_cast<size_t>(L) * rows * (n | 1)) * sizeof(float2);
-                if (n % rows == 0 && lds <= static_cast<size_t>(kMaxLds) / 2) {
+                if (n % rows == 0 && lds <= static_cast<size_t>(kMaxLds) / 4) {
                     plan->fold_all_rows[r] = rows;
                     plan->fold_all_lds[r] = lds;
                     break;
@@ -747,7 +750,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         for (int j2 = j1 + 1; j2 < plan->rb; ++j2) {
             const size_t n2 = static_cast<size_t>(g.PM >> j2);
             tmp_c = std::max(tmp_c, static_cast<size_t>(L) * n2 * n2);
-            part_n = std::max(part_n, static_cast<size_t>(L) * n2);
+            part_n = std::max(part_n, static_cast<size_t>(L) * L * n2);   // every theta1's partials
         }
         const int j2f = std::max(j1 + 1, plan->rb);
         plan->hg_j2first[j1] = j2f;
@@ -763,15 +766,21 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         plan->hg_threads[j1] = default_threads(static_cast<size_t>(g.PM >> j2f) * (g.PN >> j2f));
         if (plan->hg_lds[j1] > static_cast<size_t>(kMaxLds)) return too_big("k_o2 (global spectrum)", j1);
         plan->hg_threads[j1] = fill_cu(plan->hg_threads[j1], plan->hg_lds[j1]);
-        // one workgroup per batch: the batches of an item fold from the same H, which one XCD's
-        // L2 then serves (one workgroup per item re-read it from HBM once per batch)
+        // the batches of an item split over kHgSplit workgroups on one XCD: they fold from the same
+        // H, which that XCD's L2 then serves (one workgroup per item re-reads it from HBM once per
+        // batch; one workgroup per batch repeats the table set-up 10x at c5: measured 1 / 3 / 6 /
+        // 10 workgroups per item, c5 29.66 / 29.08 / 29.35 / 30.09 ms)
         int nbatch = 0;
         for (int j2 = j2f; j2 < J; ++j2) {
             const int pb = paths_per_batch(bcap, pslot(j2), L);
             nbatch += (L + pb - 1) / pb;
         }
-        plan->hg_lay[j1].nsplit = nbatch;
-        if (const char* e = diag_env("WST_HG_SPLIT")) plan->hg_lay[j1].nsplit = std::max(1, std::atoi(e));
+        plan->hg_lay[j1].nsplit = std::min(nbatch, kHgSplit);
+        if (const char* e = diag_env("WST_HG_SPLIT")) {   // "n0,n1,...": per j1 (last one repeats)
+            const char* q = e;
+            for (int k = 0; k < j1 && std::strchr(q, ','); ++k) q = std::strchr(q, ',') + 1;
+            plan->hg_lay[j1].nsplit = std::max(1, std::atoi(q));
+        }
     }
     if (plan->rb > 0) {
         plan->ws_tmp = wsp;
@@ -849,8 +858,15 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     plan->o2x_threads.assign(J, 64);
     bool export_on = true;
     if (const char* e = diag_env("WST_O2_EXPORT")) export_on = std::atoi(e) != 0;
-    if (const char* e = diag_env("WST_FOLD_ALL"))
-        if (std::atoi(e) == 0) std::fill(plan->fold_all_rows.begin(), plan->fold_all_rows.end(), 0);
+    if (const char* e = diag_env("WST_FOLD_ALL")) {   // 0: per-pair passes; r > 0: r rows per workgroup
+        const int r = std::atoi(e);
+        for (int k = 0; k < plan->rb; ++k) {
+            if (plan->fold_all_rows[k] == 0) continue;
+            const size_t n = static_cast<size_t>(g.PM >> k);
+            plan->fold_all_rows[k] = r;
+            plan->fold_all_lds[k] = (n + static_cast<size_t>(L) * std::max(r, 1) * (n | 1)) * sizeof(float2);
+        }
+    }
     for (int j1 = plan->rb; j1 + 1 < J && max_order >= 2; ++j1) {
         const int nM1 = g.PM >> j1, nN1 = g.PN >> j1, hld = nN1 / 2 + 1;
         if (!export_on || plan->sq || g.PM != g.PN || plan->fam_m == 0 || plan->fam_m != plan->fam_n ||
@@ -873,6 +889,11 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         plan->o2x_lds[j1] = lds;
         plan->o2x_threads[j1] = fill_cu(default_threads(static_cast<size_t>(nM1) * nN1), lds, 768);
         plan->o1_lay[j1].export_full = 1;
+        // one workgroup per item: splitting its batches over 2 / 4 workgroups of one XCD (as the
+        // HG launches after staged levels do) measured slower here (f3 k_o2 1.57 -> 1.67 / 1.66 ms,
+        // c1 1.50 -> 1.62): H is 21-75 KB, not the 0.15-0.6 MB of a staged level
+        plan->o2x_lay[j1].nsplit = 1;
+        if (const char* e = diag_env("WST_O2X_SPLIT")) plan->o2x_lay[j1].nsplit = std::max(1, std::atoi(e));
     }
     for (int j1 = plan->rb; j1 < J; ++j1) {
         plan->o1_threads[j1] = fill_cu(plan->o1_threads[j1], plan->o1_lds[j1]);
@@ -982,7 +1003,8 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
     if (!do2) return WST_OK;
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
     if (plan->o2_export[j1]) {   // spectrum exported fully transformed: fold from HBM
-        plan->ops->o2(136, 0, 1, Launch{dim3(nimg * g.L), dim3(plan->o2x_threads[j1]), plan->o2x_lds[j1], stream},
+        plan->ops->o2(136, 0, 1, Launch{dim3(nimg * g.L * std::max(1, plan->o2x_lay[j1].nsplit)),
+                                        dim3(plan->o2x_threads[j1]), plan->o2x_lds[j1], stream},
                       plan->dp, plan->o2x_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j1 + 1);
         WST_HIP_CHECK(hipGetLastError());
         return timer.end(stream, 1 + g.J + j1);
@@ -1114,15 +1136,16 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
                 B2->rows(true, Launch{dim3(n2 / f.rows, nimg), tb, flds, stream}, dp, f);
                 BigArgs m2 = args(kColModLp, j2);
                 m2.dst = tmp;
-                m2.vpart = part;
-                m2.csum = csum;
+                m2.vpart = part + static_cast<size_t>(l1) * nimg * L * n2 * plan->oms;
+                m2.csum = csum + static_cast<size_t>(l1) * nimg * L * n2;
                 m2.scale = 1.f / (static_cast<float>(n1) * static_cast<float>(n1));
                 m2.gnat = gnat(j2, 0);
                 B2->cols(true, Launch{dim3((n2 + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds[j2], stream},
                          dp, m2);
-                cm.final_(Launch{dim3(nimg * L), dim3(64), 0, stream}, dp, kFinalCols, 2, n2, plan->oms,
-                          part, gnat(j2, 1), nullptr, nullptr, L, j1, l1, j2, L, img0, d_out, pooled);
             }
+            // S2 of every theta1 in one launch (l1 = -1: blockIdx.y)
+            cm.final_(Launch{dim3(nimg * L, L), dim3(64), 0, stream}, dp, kFinalCols, 2, n2, plan->oms,
+                      part, gnat(j2, 1), nullptr, nullptr, L, j1, -1, j2, L, img0, d_out, pooled);
         }
         const int j2f = plan->hg_j2first[j1];
         if (j2f < J)

@@ -442,16 +442,27 @@ __global__ void __launch_bounds__(64) k_big_final(DevParams p, int fmode, int ki
     __shared__ float S[64];
     __shared__ float red[16];
     const int arr = blockIdx.x;
+    if (l1 < 0) {
+        // every theta1 of a staged order-2 level in one launch: l1 = blockIdx.y, whose partials
+        // follow the previous theta1's (gridDim.x arrays each)
+        l1 = blockIdx.y;
+        part += static_cast<long long>(blockIdx.y) * gridDim.x * n * oms;
+    }
     const float* P = part + static_cast<long long>(arr) * n * oms;
     const int nout = p.oM * p.oN;
-    for (int o = threadIdx.x; o < nout; o += blockDim.x) {
+    // KS lanes per output split the contraction (shuffle sum): 16 outputs (4 x 4) use every lane
+    const int KS = nout <= 16 ? 4 : nout <= 32 ? 2 : 1;
+    for (int w = threadIdx.x; w < nout * KS; w += blockDim.x) {
+        const int o = w / KS, ks = w - o * KS;
         const int ra = o / p.oN, c = o - (o / p.oN) * p.oN;
         float acc = 0.f;
         if (fmode == kFinalRows)
-            for (int k = 0; k < n; ++k) acc = fmaf(G[k * oms + ra], P[k * oms + c], acc);
+            for (int k = ks; k < n; k += KS) acc = fmaf(G[k * oms + ra], P[k * oms + c], acc);
         else
-            for (int k = 0; k < n; ++k) acc = fmaf(G[k * oms + c], P[k * oms + ra], acc);
-        S[o] = acc;
+            for (int k = ks; k < n; k += KS) acc = fmaf(G[k * oms + c], P[k * oms + ra], acc);
+        if (KS == 4) acc = wstdev::group_sum<4>(acc);
+        else if (KS == 2) acc = wstdev::group_sum<2>(acc);
+        if (ks == 0) S[o] = acc;
     }
     if (mean_out) {
         float s = 0.f;
