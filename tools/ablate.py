@@ -7,7 +7,7 @@ import os, subprocess, sys, json
 masks = {"full": 0, "no_o1_fold": 128, "no_o1_ifft": 1, "no_S1": 2, "no_U1_fft": 4, "no_o2_fold": 8,
          "no_o2_ifft": 16, "no_o2_lowpass": 64, "no_order2_paths": 8 | 16 | 64,
          "o2_only_load": 4 | 8 | 16 | 64, "no_o2_fold_s2": 256, "no_o2_fold_box": 512,
-         "no_o2_spectrum_load": 1024}
+         "no_o2_spectrum_load": 1024, "no_o2_emit": 2048}
 LIB = os.environ.get("ABL_LIB", "libwst_hip_diag.so")
 if len(sys.argv) > 1:
     masks = {k: v for k, v in masks.items() if k in sys.argv[1:]}
@@ -16,16 +16,16 @@ import os, sys, json
 sys.path.insert(0, os.getcwd())
 import numpy as np, torch, wst_amd
 from wst_amd import _lib
-B=3072
-x = torch.from_numpy(np.random.default_rng(1).integers(0,256,(B,64,64),dtype=np.uint8).astype(np.float32)/255).cuda()
-plan = _lib.Plan(64,64,4,8)
-out = torch.empty((B, plan.K, 4, 4), device="cuda")
+B, M, J = (int(v) for v in os.environ.get("WST_KM_GEOM", "3072,64,4").split(","))
+x = torch.from_numpy(np.random.default_rng(1).integers(0,256,(B,M,M),dtype=np.uint8).astype(np.float32)/255).cuda()
+plan = _lib.Plan(M,M,J,8)
+out = torch.empty((B, plan.K, plan.Mo, plan.No), device="cuda")
 wsb = plan.workspace_bytes(2048); ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 for _ in range(2): plan.forward(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st)
-acc = [0.0]*9
+acc = [0.0]*(1+2*J)
 for _ in range(3):
-    ms = plan.forward_profiled(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st, 9)
+    ms = plan.forward_profiled(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st, 1+2*J)
     acc = [a+b for a,b in zip(acc, ms)]
 print(json.dumps([a/3 for a in acc]))
 '''
