@@ -445,6 +445,12 @@ __device__ __forceinline__ void lds_lowpass(float2* U, int nb, int bs, int rows,
                                              oM, oN, S);
 }
 
+// Block-size bound of the exported-spectrum k_o2 (HG, non-SQ: f3 / c1 geometries).  A 512 bound
+// lets the compiler use 160 VGPRs instead of the 128 of a 1024 bound (f3: 11 VGPRs spilled), but
+// measured: f3 k_o2 1.53 -> 1.94-2.83 ms (256-512 threads), c1 1.50 -> 1.46; kept at 1024.
+#ifndef WST_O2X_BOUND
+#define WST_O2X_BOUND 1024
+#endif
 constexpr int kLpOM = 8;  // row stride of the GM tap matrices = largest oM of the fused path
 
 // Separable phi low-pass on the matrix cores (v_mfma_f32_16x16x4_f32: exact fp32, the fmaf chain
@@ -1485,6 +1491,9 @@ constexpr int o2_min_waves(int cap) { return cap == 48 ? 6 : cap == 24 ? 5 : 1; 
 // fully transformed half spectra in natural order, the fold reads them from HBM (no LDS copy,
 // no column FFT) and the paths start at j2first (the first LDS-resident level).
 // k_o2 body; OC > 0: the output maps are OC x OC (compile-time; the common 4 x 4 of the headline)
+#ifndef WST_HG_R
+#define WST_HG_R (HG ? 2 : 1)
+#endif
 template <int FM, int FN, int MAXN, int SQ, int HG, int OC>
 __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& p,
                                           const LdsLayout& lay, int j1, int nimg, long long img0,
@@ -1567,7 +1576,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             const long long pstride = static_cast<long long>(n1);
             const int* bx = p.box + p.box_off[j2 * J + j1] + (l2a >> 1) * (nM2 + nN2);
             if (!(dbg & 8) && !(dbg & (s2 == 2 ? 256 : 512)))
-                fold2_any<HG ? 2 : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
+                fold2_any<WST_HG_R>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
                           bx, nM2 + nN2);
             __syncthreads();
             WST_STAMP(sctr);
@@ -1599,7 +1608,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                         float* SB = reinterpret_cast<float*>(B);
                         lds_lowpass_mfma(B, npath, pslot, nM2, nN2, ld2, lpw_M(p, j2), lpw_N(p, j2),
                                          p.oMp, p.oNp, oM, oN, SB, 2 * pslot, 2);
-                        emit(SB, npath, k0, img, p.K, oM, oN, out, pooled, 2 * pslot, 2);
+                        if (!(dbg & 2048)) emit(SB, npath, k0, img, p.K, oM, oN, out, pooled, 2 * pslot, 2);
                         __syncthreads();
                     } else {
                         lds_lowpass(B, npath, pslot, nM2, nN2, ld2, tb.lpM(j2), tb.lpN(j2), tb.pmM(j2),
@@ -1637,7 +1646,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
 
 
 template <int FM, int FN, int MAXN, int SQ, int HG = 0>
-__global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, LdsLayout lay, int j1, int nimg,
+__global__ void __launch_bounds__((HG && !SQ) ? WST_O2X_BOUND : 1024, o2_min_waves(MAXN)) k_o2(DevParams p, LdsLayout lay, int j1, int nimg,
                                              long long img0, const float2* __restrict__ hexp,
                                              float* __restrict__ out, int pooled, int j2first) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

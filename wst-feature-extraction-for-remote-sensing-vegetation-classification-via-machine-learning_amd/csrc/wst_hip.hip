@@ -887,7 +887,8 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         if ((nM1 / 2) * hld > 8 * o1t) continue;   // k_o1's in-place split holds 8 items per thread
         plan->o2_export[j1] = 1;
         plan->o2x_lds[j1] = lds;
-        plan->o2x_threads[j1] = fill_cu(default_threads(static_cast<size_t>(nM1) * nN1), lds, 768);
+        plan->o2x_threads[j1] = std::min(fill_cu(default_threads(static_cast<size_t>(nM1) * nN1), lds, 768),
+                                         WST_O2X_BOUND);
         plan->o1_lay[j1].export_full = 1;
         // one workgroup per item: splitting its batches over 2 / 4 workgroups of one XCD (as the
         // HG launches after staged levels do) measured slower here (f3 k_o2 1.57 -> 1.67 / 1.66 ms,
