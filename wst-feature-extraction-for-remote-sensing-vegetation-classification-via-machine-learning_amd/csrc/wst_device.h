@@ -490,21 +490,30 @@ __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int 
         const float2* urow = Ub + (pok ? p : rows - 1) * ld;
         const float* gcol = GN + nt * 16 + li;
         f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-        for (int q0 = 0; q0 < cols; q0 += 4 * KU) {
+        // whole blocks of KU steps, then the remaining K steps one by one: no MFMA is issued on
+        // an all-padding step (68 = 17 x 4: 17 steps, not the 20 of five 16-wide blocks)
+        int q0 = 0;
+        for (; q0 + 4 * KU <= cols; q0 += 4 * KU) {
             float a[KU], bv[KU];
 #pragma unroll
             for (int u = 0; u < KU; ++u) {
                 const int q = q0 + 4 * u + lk;
-                const bool ok = q < cols;
-                const int qc = ok ? q : 0;
-                a[u] = (ok && pok) ? urow[qc].x : 0.f;
-                bv[u] = ok ? gcol[qc * oNp] : 0.f;
+                a[u] = pok ? urow[q].x : 0.f;
+                bv[u] = gcol[q * oNp];
             }
 #pragma unroll
             for (int u = 0; u < KU; u += 2) {
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[u], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u + 1], bv[u + 1], acc1, 0, 0, 0);
             }
+        }
+        for (; q0 < cols; q0 += 4) {
+            const int q = q0 + lk;
+            const bool ok = q < cols;
+            const int qc = ok ? q : 0;
+            const float a = (ok && pok) ? urow[qc].x : 0.f;
+            const float bv = ok ? gcol[qc * oNp] : 0.f;
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc0, 0, 0, 0);
         }
         const int c = nt * 16 + li;
 #pragma unroll
@@ -525,21 +534,28 @@ __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int 
         const bool cok = c < oN;
         const float* gcol = GM + at * 16 + li;
         f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-        for (int p0 = 0; p0 < rows; p0 += 4 * KU) {
+        int p0 = 0;
+        for (; p0 + 4 * KU <= rows; p0 += 4 * KU) {
             float a[KU], bv[KU];
 #pragma unroll
             for (int u = 0; u < KU; ++u) {
                 const int pp = p0 + 4 * u + lk;
-                const bool ok = pp < rows;
-                const int pc = ok ? pp : 0;
-                a[u] = ok ? gcol[pc * oMp] : 0.f;
-                bv[u] = (ok && cok) ? Ub[pc * ld + c].y : 0.f;
+                a[u] = gcol[pp * oMp];
+                bv[u] = cok ? Ub[pp * ld + c].y : 0.f;
             }
 #pragma unroll
             for (int u = 0; u < KU; u += 2) {
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[u], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u + 1], bv[u + 1], acc1, 0, 0, 0);
             }
+        }
+        for (; p0 < rows; p0 += 4) {
+            const int pp = p0 + lk;
+            const bool ok = pp < rows;
+            const int pc = ok ? pp : 0;
+            const float a = ok ? gcol[pc * oMp] : 0.f;
+            const float bv = (ok && cok) ? Ub[pc * ld + c].y : 0.f;
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, bv, acc0, 0, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
