@@ -461,7 +461,9 @@ constexpr int kLpOM = 8;  // row stride of the GM tap matrices = largest oM of t
 //      slots of row p of U (c < oN);
 //   2. S[a][c] = sum_p GM[p][a] T[p][c]      (oMp x rows) . (rows x oNp)  -> S (nb x oM x oN).
 // U real in .x (row stride ld, array stride bs), in the physical order the tap matrices were
-// built for.  GM / GN: global (L2-resident) tap matrices, rows zero-padded to oMp / oNp (x16).
+// built for.  GM / GN: global (L2-resident) tap matrices, columns zero-padded to oMp / oNp (x16),
+// in MFMA operand order (wst_hip.hip: 16-row blocks of 64 lanes x 4 K steps, then the tail rows
+// row-major).
 // One wave per 16 x 16 output tile, K in steps of 4 x KU (loads of a step issued together, two
 // accumulators alternate so consecutive MFMAs do not wait on each other).  Lane map of the
 // 16x16x4 form: A[m = lane & 15][k = lane >> 4], B[k = lane >> 4][n = lane & 15],
@@ -488,24 +490,23 @@ __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int 
         const int p = mt * 16 + li;
         const bool pok = p < rows;
         const float2* urow = Ub + (pok ? p : rows - 1) * ld;
-        const float* gcol = GN + nt * 16 + li;
+        const int nfb = cols >> 4;
+        const float4* gblk = reinterpret_cast<const float4*>(GN) + nt * 64 + lane;
+        const float* gcol = GN + nfb * nnt * 256 - 16 * nfb * oNp + nt * 16 + li;   // tail rows
         f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-        // whole blocks of KU steps, then the remaining K steps one by one: no MFMA is issued on
-        // an all-padding step (68 = 17 x 4: 17 steps, not the 20 of five 16-wide blocks)
+        // whole 16-row K blocks (one 16-byte tap load per lane feeds 4 MFMAs), then the remaining
+        // K steps one by one: no MFMA is issued on an all-padding step (68 = 17 x 4: 17 steps, not
+        // the 20 of five 16-wide blocks)
         int q0 = 0;
-        for (; q0 + 4 * KU <= cols; q0 += 4 * KU) {
-            float a[KU], bv[KU];
+        for (int blk = 0; blk < nfb; ++blk, q0 += 4 * KU) {
+            const float4 b4 = gblk[blk * nnt * 64];
+            float a[KU];
 #pragma unroll
-            for (int u = 0; u < KU; ++u) {
-                const int q = q0 + 4 * u + lk;
-                a[u] = pok ? urow[q].x : 0.f;
-                bv[u] = gcol[q * oNp];
-            }
-#pragma unroll
-            for (int u = 0; u < KU; u += 2) {
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[u], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u + 1], bv[u + 1], acc1, 0, 0, 0);
-            }
+            for (int u = 0; u < KU; ++u) a[u] = pok ? urow[q0 + 4 * u + lk].x : 0.f;
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b4.x, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b4.y, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b4.z, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b4.w, acc1, 0, 0, 0);
         }
         for (; q0 < cols; q0 += 4) {
             const int q = q0 + lk;
@@ -532,22 +533,20 @@ __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int 
         const float2* Ub = U + b * bs;
         const int c = ct * 16 + li;
         const bool cok = c < oN;
-        const float* gcol = GM + at * 16 + li;
+        const int nfb = rows >> 4;
+        const float4* gblk = reinterpret_cast<const float4*>(GM) + at * 64 + lane;
+        const float* gcol = GM + nfb * nat * 256 - 16 * nfb * oMp + at * 16 + li;   // tail rows
         f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
         int p0 = 0;
-        for (; p0 + 4 * KU <= rows; p0 += 4 * KU) {
-            float a[KU], bv[KU];
+        for (int blk = 0; blk < nfb; ++blk, p0 += 4 * KU) {
+            const float4 a4 = gblk[blk * nat * 64];
+            float bv[KU];
 #pragma unroll
-            for (int u = 0; u < KU; ++u) {
-                const int pp = p0 + 4 * u + lk;
-                a[u] = gcol[pp * oMp];
-                bv[u] = cok ? Ub[pp * ld + c].y : 0.f;
-            }
-#pragma unroll
-            for (int u = 0; u < KU; u += 2) {
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[u], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u + 1], bv[u + 1], acc1, 0, 0, 0);
-            }
+            for (int u = 0; u < KU; ++u) bv[u] = cok ? Ub[(p0 + 4 * u + lk) * ld + c].y : 0.f;
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, bv[0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, bv[1], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, bv[2], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.w, bv[3], acc1, 0, 0, 0);
         }
         for (; p0 < rows; p0 += 4) {
             const int pp = p0 + lk;

@@ -572,6 +572,9 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     // wide tap matrices for the MFMA low-pass (lds_lowpass_mfma), columns padded to x16:
     //   [2r + d] level r in physical order (r < J), [2J + d] level 0 in natural order (k_prep)
     const int oMp = (g.oM + 15) & ~15, oNp = (g.oN + 15) & ~15;
+    // Stored in the MFMA operand order: each 16-row K block of a 16-column tile is 64 lanes x 4
+    // K steps (lane = 16 (q & 3) + column, the 4 values of a lane contiguous: one 16-byte load
+    // feeds 4 MFMAs); rows past the last whole block follow row-major.
     std::vector<float> lpw;
     std::vector<int> lpw_off(2 * static_cast<size_t>(J + 1), 0);
     for (int slot = 0; slot <= J; ++slot)
@@ -582,12 +585,20 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
             const int sdec = 1 << (J - r);
             const auto& h = d == 0 ? fb.hM[r] : fb.hN[r];
             const int* pm = perm.data() + t.perm_off[2 * r + d];
-            lpw_off[2 * slot + d] = static_cast<int>(lpw.size());
-            for (int q = 0; q < n; ++q) {
+            const auto tap = [&](int q, int a) {
                 const int phys = slot < J ? pm[q] : q;
-                for (int a = 0; a < np_; ++a)
-                    lpw.push_back(a < no ? static_cast<float>(h[((sdec * (a + 1) - phys) % n + n) % n]) : 0.f);
-            }
+                return a < no ? static_cast<float>(h[((sdec * (a + 1) - phys) % n + n) % n]) : 0.f;
+            };
+            while (lpw.size() % 4) lpw.push_back(0.f);
+            lpw_off[2 * slot + d] = static_cast<int>(lpw.size());
+            const int nfb = n / 16, ntile = np_ / 16;
+            for (int b = 0; b < nfb; ++b)
+                for (int tl = 0; tl < ntile; ++tl)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int u = 0; u < 4; ++u)
+                            lpw.push_back(tap(16 * b + 4 * u + (lane >> 4), 16 * tl + (lane & 15)));
+            for (int q = 16 * nfb; q < n; ++q)
+                for (int a = 0; a < np_; ++a) lpw.push_back(tap(q, a));
         }
     // twiddles exp(-2 pi i k / n) per level and side; pool order: M levels 0..J, then N levels
     std::vector<float2> tw;
