@@ -171,13 +171,24 @@ def src_sha():
     return h.hexdigest()[:16]
 
 
-def pmc_traffic(sha, kernel):
-    """HBM bytes per launch of `kernel` from committed rocprofv3 PMC passes of this exact build."""
+def pmc_file_config(name):
+    """Config a PMC summary file belongs to: profiles/pmc_<tag>_<config>.json (tools/profile_cfg.sh);
+    the suffix-less pmc_<tag>.json of tools/profile_round.sh is the default config c2."""
+    stem = name[len("pmc_"):-len(".json")]
+    last = stem.rsplit("_", 1)[-1]
+    return last if last in CONFIGS else "c2"
+
+
+def pmc_traffic(sha, kernel, config="c2"):
+    """HBM bytes per launch of `kernel` from committed rocprofv3 PMC passes of this exact build and
+    geometry.  Kernel names repeat across geometries (c5's LDS-resident levels instantiate the same
+    k_o2<3, 3, 136, ...> as c2), so only files of this config count; c3 / c4 run c2's kernels."""
     pdir = os.path.join(ROOT, "profiles")
     if not os.path.isdir(pdir):
         return None
+    want = "c2" if config in ("c3", "c4") else config
     for name in sorted(os.listdir(pdir), reverse=True):
-        if name.startswith("pmc_") and name.endswith(".json"):
+        if name.startswith("pmc_") and name.endswith(".json") and pmc_file_config(name) == want:
             try:
                 d = json.load(open(os.path.join(pdir, name)))
             except Exception:
@@ -552,7 +563,7 @@ def main():
         "bound": "valu", "pipe": "fp32 VALU (LDS FFT butterflies; f32 MFMA only in the wide low-pass)",
         "kernel": f"{dom} ({dname}, ...>)", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
-        "traffic": pmc_traffic(sha, dname) or pmc_traffic(lib_sha(), dname),
+        "traffic": pmc_traffic(sha, dname, args.config) or pmc_traffic(lib_sha(), dname, args.config),
         "launches_per_step": nchunks,
         "avg_launch_ms": round(kms[dom] / nchunks, 4),
         "alg_flop_per_launch": round(dom_flop / nchunks),

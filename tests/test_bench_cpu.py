@@ -72,3 +72,22 @@ def test_patchgen_is_keyed_by_global_index():
     # uniform bytes: mean ~127.5
     big = patchgen.generate_patches_u8(1, 0, 64, 3, 64, 64)
     assert abs(big.mean() - 127.5) < 1.0
+
+
+def test_pmc_traffic_is_looked_up_per_config(tmp_path, monkeypatch):
+    # c5's LDS-resident levels instantiate the same k_o2<3, 3, 136, ...> as c2: a c5 PMC file must
+    # never supply c2's roofline.traffic (and vice versa)
+    assert bench.pmc_file_config("pmc_r01s12.json") == "c2"
+    assert bench.pmc_file_config("pmc_r02s4_c5.json") == "c5"
+    assert bench.pmc_file_config("pmc_r02s4_f3.json") == "f3"
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    name = "k_o2<3, 3, 136, 1, 0>"
+    for fname, v in [("pmc_x_c2.json", 111), ("pmc_x_c5.json", 555)]:
+        (prof / fname).write_text(json.dumps({"src_sha": "s", "hbm_bytes_per_launch": {name: v}}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.pmc_traffic("s", "k_o2<3, 3, 136", "c2") == 111
+    assert bench.pmc_traffic("s", "k_o2<3, 3, 136", "c3") == 111
+    assert bench.pmc_traffic("s", "k_o2<3, 3, 136", "c5") == 555
+    assert bench.pmc_traffic("s", "k_o2<3, 3, 136", "f3") is None
+    assert bench.pmc_traffic("other", "k_o2<3, 3, 136", "c2") is None
