@@ -90,6 +90,13 @@ struct DevParams {
     const float* lpw;
     const int* lpw_off;
     int oMp, oNp;
+    // k_o2r (wst_wave.h): the order-2 filters of level j2 = j1 + 1 in the kernel's lane order
+    // (per path: R x R elements x 64 lanes x 4 alias taps, floats; [j1 * L + l2], -1 = not built)
+    // and the natural-order tap matrices ([2r] GM_r, [2r + 1] GN_r; rows of 4 floats)
+    const float* psil;
+    const long long* psil_off;
+    const float* lpn;
+    const int* lpn_off;
 };
 
 // Per-launch LDS layout (byte offsets) and the table slices copied into LDS.
@@ -902,13 +909,24 @@ __host__ __device__ inline int odd_ld(int n) { return n | 1; }
 // Streaming (non-temporal) 8-byte load / store: the half-spectrum hand-off k_o1 -> k_o2 is
 // written and read once (~0.9 GB per 2048-plane chunk at the 96^2 level), kept from displacing
 // the filters the folds re-read from L2 (c2: -2.5 %, measured).
+#ifndef WST_NT_HANDOFF
+#define WST_NT_HANDOFF 1   // 0: default-policy hand-off loads / stores (A/B builds)
+#endif
 __device__ __forceinline__ float2 ldnt(const float2* p) {
+#if WST_NT_HANDOFF
     return __builtin_bit_cast(float2,
                               __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p)));
+#else
+    return *p;
+#endif
 }
 __device__ __forceinline__ void stnt(float2* p, float2 v) {
+#if WST_NT_HANDOFF
     __builtin_nontemporal_store(v.x, &p->x);
     __builtin_nontemporal_store(v.y, &p->y);
+#else
+    *p = v;
+#endif
 }
 
 // dst[i] = src[i] for i < n (global -> LDS): eight loads per thread in flight before the stores
@@ -925,7 +943,13 @@ __device__ __forceinline__ void copy_to_lds(float2* dst, const float2* __restric
         for (int i0 = threadIdx.x; i0 < n4; i0 += K * T) {
             f4v t[K];
 #pragma unroll
-            for (int k = 0; k < K; ++k) t[k] = __builtin_nontemporal_load(s4 + min(i0 + k * T, n4 - 1));
+            for (int k = 0; k < K; ++k) {
+#if WST_NT_HANDOFF
+                t[k] = __builtin_nontemporal_load(s4 + min(i0 + k * T, n4 - 1));
+#else
+                t[k] = s4[min(i0 + k * T, n4 - 1)];
+#endif
+            }
 #pragma unroll
             for (int k = 0; k < K; ++k)
                 if (i0 + k * T < n4) d4[i0 + k * T] = t[k];

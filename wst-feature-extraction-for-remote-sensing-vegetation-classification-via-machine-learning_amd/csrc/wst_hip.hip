@@ -23,6 +23,7 @@
 #include "filter_bank.h"
 #include "wst_hip.h"
 #include "wst_launch.h"
+#include "wst_wave.h"
 
 using wstdev::DevParams;
 using wstdev::LdsLayout;
@@ -155,6 +156,10 @@ struct wst_plan {
     std::vector<int> box_off_host;
     float* d_lpt = nullptr;
     int* d_lpt_off = nullptr;
+    float* d_psil = nullptr;          // k_o2r lane-ordered order-2 filters (wst_wave.h)
+    long long* d_psil_off = nullptr;
+    int* d_lpn_off = nullptr;
+    std::vector<int> o2r;             // per j1: the j2 = j1 + 1 paths run in k_o2r
     // launch geometry
     int fam_m = 0, fam_n = 0;   // FFT size families (odd part of PM / PN), 0 = generic DFT
     const FamilyOps* ops = nullptr;
@@ -225,6 +230,9 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_lpn);
     (void)hipFree(p->d_lpw);
     (void)hipFree(p->d_lpw_off);
+    (void)hipFree(p->d_psil);
+    (void)hipFree(p->d_psil_off);
+    (void)hipFree(p->d_lpn_off);
     for (auto& kv : p->ws_by_stream)
         if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     delete p;
@@ -569,6 +577,42 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                     lpn.push_back(a < no ? static_cast<float>(h[((sdec * (a + 1) - p) % n + n) % n]) : 0.f);
         }
     plan->oms = oms;
+    // k_o2r (wst_wave.h): square compiled levels N1 (96 / 48) of a plane with 4 x 4 maps, the paths
+    // j2 = j1 + 1 of level j1 held in one wave each.  Per path l2 the filter psi_{j1+1, l2} at level
+    // j1 in the kernel's lane order: element (i, k) of lane (h, g) is bin (u, v) = (8 i + rev(h),
+    // 8 k + rev(g)) of the n2 x n2 fold, its four alias taps (u, v), (u, v + n2), (u + n2, v),
+    // (u + n2, v + n2) of the N1 x N1 filter stored together (one 16-byte load).
+    plan->o2r.assign(J, 0);
+    std::vector<float> psil;
+    std::vector<long long> psil_off(static_cast<size_t>(J) * L, -1);
+    {
+        bool o2r_on = true;
+        if (const char* e = diag_env("WST_O2R")) o2r_on = std::atoi(e) != 0;
+        const FamilyOps* fops = family_ops(plan->fam_m, plan->fam_n);
+        for (int j1 = 0; j1 + 1 < J && o2r_on && max_order >= 2; ++j1) {
+            const int n1 = g.PM >> j1;
+            if (g.PM != g.PN || plan->fam_m != plan->fam_n || !fops || !wstdev::o2r_size(n1) ||
+                g.oM != 4 || g.oN != 4 || oms != 4 || std::max(g.PM, g.PN) >> j1 > wstbig::kBigMinN ||
+                j1 >= wst::psi_levels(j1 + 1, J))
+                continue;
+            plan->o2r[j1] = 1;
+            const int n2 = n1 / 2, R = n2 / 8;
+            for (int l2 = 0; l2 < L; ++l2) {
+                psil_off[static_cast<size_t>(j1) * L + l2] = static_cast<long long>(psil.size());
+                const auto& f = fb.psi[static_cast<size_t>(j1 + 1) * L + l2][j1];
+                for (int i = 0; i < R; ++i)
+                    for (int k = 0; k < R; ++k)
+                        for (int lane = 0; lane < 64; ++lane) {
+                            const int u = 8 * i + wstdev::rev3(wstdev::o2r_h(lane));
+                            const int v = 8 * k + wstdev::rev3(wstdev::o2r_g(lane));
+                            psil.push_back(static_cast<float>(f[static_cast<size_t>(u) * n1 + v]));
+                            psil.push_back(static_cast<float>(f[static_cast<size_t>(u) * n1 + v + n2]));
+                            psil.push_back(static_cast<float>(f[static_cast<size_t>(u + n2) * n1 + v]));
+                            psil.push_back(static_cast<float>(f[static_cast<size_t>(u + n2) * n1 + v + n2]));
+                        }
+            }
+        }
+    }
     // wide tap matrices for the MFMA low-pass (lds_lowpass_mfma), columns padded to x16:
     //   [2r + d] level r in physical order (r < J), [2J + d] level 0 in natural order (k_prep)
     const int oMp = (g.oM + 15) & ~15, oNp = (g.oN + 15) & ~15;
@@ -647,6 +691,9 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     if ((rc = upload(&plan->d_lpn, lpn)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_lpw, lpw)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_lpw_off, lpw_off)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_psil, psil)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_psil_off, psil_off)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_lpn_off, plan->lpn_off)) != WST_OK) return rc;
 
     DevParams& dp = plan->dp;
     dp.M = g.M; dp.N = g.N; dp.PM = g.PM; dp.PN = g.PN; dp.J = J; dp.L = L;
@@ -671,6 +718,8 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     if (const char* e = diag_env("WST_BOX1_MIN_S")) dp.box1_min_s = std::atoi(e);
     dp.lpt = plan->d_lpt; dp.lpt_off = plan->d_lpt_off;
     dp.lpw = plan->d_lpw; dp.lpw_off = plan->d_lpw_off; dp.oMp = oMp; dp.oNp = oNp;
+    dp.psil = plan->d_psil; dp.psil_off = plan->d_psil_off;
+    dp.lpn = plan->d_lpn; dp.lpn_off = plan->d_lpn_off;
     // square variant (bounded FFT sizes + fused order-2 low-pass): square plane of a compiled
     // family, oM <= kLpOM and every order-2 level's column units hold ceil(oM / 2) slots
     plan->sq = (plan->fam_m > 0 && plan->fam_m == plan->fam_n && g.PM == g.PN &&
@@ -1014,6 +1063,17 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
     if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
     if (!do2) return WST_OK;
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
+    int j2first = j1 + 1;
+    if (plan->o2r[j1]) {   // the j2 = j1 + 1 paths in registers (k_o2r), the rest in k_o2
+        const int n1 = g.PM >> j1;
+        if (!plan->ops->o2r(n1, Launch{dim3(nimg * g.L), dim3(64 * wstdev::kO2rWaves),
+                                       static_cast<size_t>(wstdev::o2r_lds(n1)), stream},
+                            plan->dp, j1, nimg, img0, hexp, d_out, pooled))
+            return fail(WST_ERR_UNSUPPORTED, "k_o2r not compiled for level size " + std::to_string(n1));
+        WST_HIP_CHECK(hipGetLastError());
+        j2first = j1 + 2;
+        if (j2first >= g.J) return timer.end(stream, 1 + g.J + j1);
+    }
     if (plan->o2_export[j1]) {   // spectrum exported fully transformed: fold from HBM
         plan->ops->o2(136, 0, 1, Launch{dim3(nimg * g.L * std::max(1, plan->o2x_lay[j1].nsplit)),
                                         dim3(plan->o2x_threads[j1]), plan->o2x_lds[j1], stream},
@@ -1023,7 +1083,7 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
     }
     plan->ops->o2(plan->cap[j1], plan->sq, 0,
                   Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
-                  plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j1 + 1);
+                  plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j2first);
     WST_HIP_CHECK(hipGetLastError());
     return timer.end(stream, 1 + g.J + j1);
 }

@@ -13,6 +13,8 @@ namespace {
 
 constexpr int FM = WST_FAM_M, FN = WST_FAM_N;
 constexpr bool kSquareFamily = (FM == FN) && FM > 0;
+// k_o2r level sizes 96 and 48 (wst_wave.h) belong to family 3
+constexpr bool kO2r = kSquareFamily && FM == 3;
 
 template <int C, int SQ>
 hipError_t attrs_cap() {
@@ -42,8 +44,17 @@ hipError_t set_attrs() {
         if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2<FM, FN, 136, 0, 1>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds)) != hipSuccess)
             return e;
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2<FM, FN, 136, 1, 1>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds);
+        if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2<FM, FN, 136, 1, 1>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds)) != hipSuccess)
+            return e;
+        if constexpr (kO2r) {
+            if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2r<FM, 96>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds)) != hipSuccess)
+                return e;
+            if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2r<FM, 48>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds)) != hipSuccess)
+                return e;
+        }
     }
     return hipSuccess;
 }
@@ -103,12 +114,30 @@ void o2(int cap, int sq, int hg, const Launch& q, const DevParams& dp, const Lds
     o2_sq<0, 0>(cap, q, dp, lay, j1, nimg, img0, hexp, out, pooled, j2first);
 }
 
+bool o2r(int n1c, const Launch& q, const DevParams& dp, int j1, int nimg, long long img0,
+         const float2* hexp, float* out, int pooled) {
+    if constexpr (kO2r) {
+        if (n1c == 96) {
+            hipLaunchKernelGGL((wstdev::k_o2r<FM, 96>), q.grid, q.block, q.lds, q.st, dp, j1, nimg, img0, hexp,
+                               out, pooled);
+            return true;
+        }
+        if (n1c == 48) {
+            hipLaunchKernelGGL((wstdev::k_o2r<FM, 48>), q.grid, q.block, q.lds, q.st, dp, j1, nimg, img0, hexp,
+                               out, pooled);
+            return true;
+        }
+    }
+    (void)n1c; (void)q; (void)dp; (void)j1; (void)nimg; (void)img0; (void)hexp; (void)out; (void)pooled;
+    return false;
+}
+
 }  // namespace
 
 #define WST_GETTER_NAME(A, B) WST_FAMILY_GETTER(A, B)
 #define WST_GETTER_EXPAND(A, B) WST_GETTER_NAME(A, B)
 const FamilyOps& WST_GETTER_EXPAND(WST_FAM_M, WST_FAM_N)() {
-    static const FamilyOps ops{FM, FN, set_attrs, prep, o1, o2};
+    static const FamilyOps ops{FM, FN, set_attrs, prep, o1, o2, o2r};
     return ops;
 }
 

@@ -7,6 +7,7 @@
 
 #include "wst_device.h"
 #include "wst_staged.h"
+#include "wst_wave.h"
 
 namespace wstlaunch {
 
@@ -31,6 +32,10 @@ struct FamilyOps {
     // hg: spectrum of a big level read from HBM (square families, cap 136), paths from j2first
     void (*o2)(int cap, int sq, int hg, const Launch&, const DevParams&, const LdsLayout&, int j1,
                int nimg, long long img0, const float2* hexp, float* out, int pooled, int j2first);
+    // k_o2r (wst_wave.h): the j2 = j1 + 1 paths of an n1c x n1c level in registers; false when this
+    // family has no k_o2r for n1c (nothing launched)
+    bool (*o2r)(int n1c, const Launch&, const DevParams&, int j1, int nimg, long long img0,
+                const float2* hexp, float* out, int pooled);
 };
 
 // HBM-staged passes of one big level size N (wst_staged.h), compiled per N (wst_staged.hip).
