@@ -208,7 +208,12 @@ def pmc_traffic(sha, kernel, config="c2"):
 # ------------------------------------------------------------------------------------------
 def cpu_workers():
     """Host cores this process may use: the affinity set, capped by OMP_NUM_THREADS when the
-    environment sets one (the GPU box sets 16 = one GPU's share of the host)."""
+    environment sets one (the GPU box sets 16 = one GPU's share of the host).  Ranks started by
+    launch_ranks inherit the parent's count in WST_CPU_WORKERS: torch.distributed.run sets
+    OMP_NUM_THREADS=1 in every rank when nproc > 1, which is not the host's core budget."""
+    inherited = os.environ.get("WST_CPU_WORKERS")
+    if inherited and inherited.isdigit() and int(inherited) > 0:
+        return int(inherited)
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     omp = os.environ.get("OMP_NUM_THREADS")
     if omp and omp.isdigit() and int(omp) > 0:
@@ -324,6 +329,7 @@ def launch_ranks(n):
            os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("WST_CPU_WORKERS", str(cpu_workers()))   # the parent's budget, not torchrun's 1
     return subprocess.call(cmd, env=env)
 
 
@@ -375,27 +381,39 @@ def launch_check(args, rank, world):
         sys.exit(1)
 
 
-def c3_check(cfg, feats, lo, hi, nsample=8):
-    """Recreate `nsample` sampled patches of this rank's shard on the host (oracle/patchgen.py)
-    and compare their pooled features with the float64 oracle (per-feature max-normalised)."""
+def c3_check(cfg, rows, lo, hi, full_output=False, nsample=8, seed=C3_SEED):
+    """Recreate `nsample` sampled patches of the global range [lo, hi) on the host
+    (oracle/patchgen.py) and compare their rows of `rows` (row i - lo = patch i: pooled features, or
+    the full (C, K, Mo, No) maps) with the float64 oracle, per feature / coefficient max-normalised.
+    After an all-gather [lo, hi) is the whole job, so other ranks' shards are checked too."""
     import numpy as np
     from oracle import kymatio_ref as kr
     from oracle import patchgen
-    idx = np.random.default_rng(77).choice(cfg["total"], 64 * nsample, replace=False)
+    idx = np.random.default_rng(77).choice(cfg["total"], min(cfg["total"], 64 * nsample), replace=False)
     mine = [int(i) for i in idx if lo <= i < hi][:nsample]
     if not mine:
         return 0.0, 0
     sc = kr.Scattering2D(J=cfg["J"], shape=(cfg["M"], cfg["N"]), L=cfg["L"])
     ref, got = [], []
     for i in mine:
-        u8 = patchgen.generate_patches_u8(C3_SEED, i, 1, cfg["C"], cfg["M"], cfg["N"])[0]
-        ref.append(kr.extract_wst_features(u8.astype(np.float32) / 255, J=cfg["J"], L=cfg["L"],
-                                           scattering=sc))
-        got.append(feats[(i - lo) * cfg["C"]:(i - lo + 1) * cfg["C"]].reshape(-1).cpu().numpy())
+        u8 = patchgen.generate_patches_u8(seed, i, 1, cfg["C"], cfg["M"], cfg["N"])[0]
+        x = u8.astype(np.float32) / 255
+        if full_output:
+            S = sc(x)                                               # (C, K, Mo, No)
+            ref.append(S.reshape(S.shape[0] * S.shape[1], -1))       # per (channel, coefficient)
+            got.append(rows[i - lo].cpu().numpy().reshape(ref[-1].shape))
+        else:
+            ref.append(kr.extract_wst_features(x, J=cfg["J"], L=cfg["L"], scattering=sc))
+            got.append(rows[i - lo].reshape(-1).cpu().numpy())
     ref, got = np.stack(ref), np.stack(got).astype(np.float64)
-    scale = np.abs(ref).max(axis=0)
+    if full_output:   # per coefficient: max |d| / max |S| over the sampled patches and positions
+        scale = np.abs(ref).max(axis=(0, 2))
+        err = np.abs(got - ref).max(axis=(0, 2))
+    else:
+        scale = np.abs(ref).max(axis=0)
+        err = np.abs(got - ref).max(axis=0)
     scale = np.where(scale > 0, scale, 1.0)
-    return float((np.abs(got - ref).max(axis=0) / scale).max()), len(mine)
+    return float((err / scale).max()), len(mine)
 
 
 def main():
@@ -407,6 +425,12 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="patches per GPU (default: config)")
     ap.add_argument("--pooled", action="store_true", help="fused mean/std epilogue output")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL all-gather of features")
+    ap.add_argument("--c3-output", choices=("pooled", "full"), default="pooled",
+                    help="c3: gather pooled features (10 GB at 1M) or the full coefficient tensor "
+                         "(N, 3, 417, 4, 4) (80 GB at 1M)")
+    ap.add_argument("--c3-gather", choices=("all", "root"), default="all",
+                    help="c3: all-gather to every rank, or gather to rank 0")
+    ap.add_argument("--c3-total", type=int, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-budget", type=float, default=8.0, help="seconds per CPU-baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-probes", action="store_true", help="skip the BW / FP32 probe kernels")
@@ -486,27 +510,38 @@ def main():
         extra["sweep"] = [f"{t}_{i}" for t, i in NOISE_SWEEP]
     elif args.config == "c3":
         from wst_amd import distributed as wdist
+        if args.c3_total:
+            cfg["total"] = args.c3_total
         total = cfg["total"]
-        lo, hi = wdist.shard_range(total, rank, world)
-        mine = hi - lo
-        feats = torch.empty((mine * C, 2 * K), dtype=torch.float32, device=dev)
+        full_out = args.c3_output == "full"
+        row = C * K * Mo * No if full_out else C * 2 * K
+        # receive / shard buffers allocated once, outside the timed step; the plan writes each
+        # batch's outputs straight into this rank's rows of the gather's send buffer
+        sg = wdist.ShardGather(total, (row,), torch.float32, dev, root_only=args.c3_gather == "root")
+        lo, hi, mine = sg.lo, sg.hi, sg.mine
         xb = torch.empty((B, C, M, N), dtype=torch.float32, device=dev)
 
+        def gen(first, nb):
+            # patches first .. first + nb - 1 of the job, keyed by global index
+            _lib.check_aux(lib.wst_patch_generate(C3_SEED, first, nb, C, M, N, 1, xb.data_ptr(), stream))
+            return xb
+
+        def comp(xin, nb, rows):
+            plan.forward(xin.data_ptr(), nb * C, rows.data_ptr(), not full_out, ws.data_ptr(), ws_bytes, stream)
+
+        result = [None]
+
         def step():  # noqa: F811
-            for b0 in range(0, mine, B):
-                nb = min(B, mine - b0)
-                # patches lo + b0 .. lo + b0 + nb - 1 of the job, keyed by global index
-                _lib.check_aux(lib.wst_patch_generate(C3_SEED, lo + b0, nb, C, M, N, 1, xb.data_ptr(),
-                                                      stream))
-                plan.forward(xb.data_ptr(), nb * C, feats[b0 * C:].data_ptr(), True, ws.data_ptr(),
-                             ws_bytes, stream)
-            if world > 1:   # RCCL all-gather of every rank's pooled features (padded shards)
-                wdist.gather_shards(feats.view(mine, C * 2 * K), total)
+            result[0] = wdist.run_sharded_job(sg, B, gen, comp)
         units_per_step = mine
         scaling = "strong"
-        c3_state = (feats, lo, hi)
-        extra["c3"] = {"total_patches": total, "patches_this_rank": mine,
-                       "gathered_bytes": total * C * 2 * K * 4 if world > 1 else 0}
+        c3_state = (sg, result, full_out)
+        extra["c3"] = {"total_patches": total, "patches_this_rank": mine, "output": args.c3_output,
+                       "bytes_per_patch": row * 4,
+                       "collective": ("none (one rank)" if world == 1 else
+                                      "RCCL all_gather_into_tensor (equal shards: no compaction)"
+                                      if args.c3_gather == "all" else "RCCL gather to rank 0"),
+                       "gathered_bytes": sg.bytes_moved()}
 
     for _ in range(args.warmup):
         step()
@@ -527,13 +562,18 @@ def main():
         dt = t.item()
     ms_per_step = dt / args.steps * 1e3
     if args.config == "c3":
-        value = cfg["total"] * args.steps / dt
+        value = total * args.steps / dt
     else:
         value = units_per_step * world * args.steps / dt
 
-    if c3_state is not None:        # sampled patches of every shard vs the float64 oracle
-        err, nchk = c3_check(cfg, *c3_state)
-        if world > 1:
+    if c3_state is not None:        # sampled patches vs the float64 oracle
+        sg, result, full_out = c3_state
+        gathered = result[0] is not None and (world == 1 or sg.full is not None)
+        if gathered:
+            err, nchk = c3_check(cfg, result[0], 0, total, full_out)    # the gathered job
+        else:
+            err, nchk = c3_check(cfg, sg.local, lo, hi, full_out)       # this rank's shard
+        if world > 1 and not (gathered and args.c3_gather == "all"):
             t = torch.tensor([err, float(nchk)], dtype=torch.float64, device=dev)
             e2 = t.clone()
             dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
@@ -608,11 +648,13 @@ def main():
             "data": "synthetic uint8/255 RGB patches (load_rgb_image distribution), resident in HBM",
             "config": {"workload": cfg["workload"], "patches_per_gpu": units_per_step, "channels": C,
                        "shape": [M, N], "J": J, "L": L, "max_order": 2, "K": K,
-                       "output": ("pooled [mean|std]" if (args.pooled or args.config in ("c3", "c4"))
+                       "output": ("pooled [mean|std]" if (args.pooled or args.config == "c4" or
+                                                       (args.config == "c3" and args.c3_output == "pooled"))
                                   else f"full ({K},{Mo},{No}) fp32"),
                        "parallelism": f"patch-sharded x{world} (no collective in step)"
                                       if args.config != "c3" else
-                                      f"patch-sharded x{world} + RCCL all-gather of pooled features"},
+                                      f"patch-sharded x{world} + RCCL {'all-gather' if args.c3_gather == 'all' else 'gather'}"
+                                      f" of {'the coefficient tensor' if args.c3_output == 'full' else 'pooled features'}"},
             "roofline": roofline, "step_roofline": step_roof, "measured": probes, "cpu_baseline": cpu,
         }
         if gather:

@@ -53,8 +53,21 @@ def test_golden_parity_numpy_frontend(name):
         if e.code == _lib.WST_ERR_UNSUPPORTED:
             pytest.skip(f"{name}: not yet covered by the HIP path: {e}")
         raise
-    assert S.shape == d["S"].shape and S.dtype == np.float32
+    assert S.shape == d["S"].shape and S.dtype == np.float64   # kymatio.numpy returns float64
     assert_parity(S, d["S"], TOL, name)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_numpy_frontend_dtype_contract(dtype):
+    # kymatio.numpy multiplies by float64 filters: float32 input (train_and_save_model.py:51-56,368)
+    # and float64 input both come back float64; the torch frontend keeps float32 on the device
+    d, x = golden_input("c2_rgb64_J4_L8")
+    s = NpS(J=4, shape=(64, 64), L=8)
+    S = s(x.astype(dtype))
+    assert S.dtype == np.float64 and S.shape == d["S"].shape
+    assert_parity(S, d["S"], TOL, "c2 dtype " + np.dtype(dtype).name)
+    F = s.pooled(x.astype(dtype))
+    assert F.dtype == np.float64 and F.shape == (3, 2 * 417)
 
 
 @pytest.mark.parametrize("name", ["c2_rgb64_J4_L8", "c1_rgb64_J2_L8"])

@@ -577,39 +577,49 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                     lpn.push_back(a < no ? static_cast<float>(h[((sdec * (a + 1) - p) % n + n) % n]) : 0.f);
         }
     plan->oms = oms;
-    // k_o2r (wst_wave.h): square compiled levels N1 (96 / 48) of a plane with 4 x 4 maps, the paths
-    // j2 = j1 + 1 of level j1 held in one wave each.  Per path l2 the filter psi_{j1+1, l2} at level
-    // j1 in the kernel's lane order: element (i, k) of lane (h, g) is bin (u, v) = (8 i + rev(h),
-    // 8 k + rev(g)) of the n2 x n2 fold, its four alias taps (u, v), (u, v + n2), (u + n2, v),
-    // (u + n2, v + n2) of the N1 x N1 filter stored together (one 16-byte load).
+    // k_o2r (wst_wave.h): square compiled levels N1 (96 / 48) of a plane with 4 x 4 maps, every
+    // order-2 path j2 = j1 + d (d = 1 .. o2r_depth, n2 = N1 >> d) held in one wave.  Per path
+    // (j2, l2) the filter psi_{j2, l2} at level j1 in the kernel's lane order: element (i, k) of lane
+    // (h, g) of the G x G grid is bin (u, v) = (G i + rev(h), G k + rev(g)) of the n2 x n2 fold, its
+    // taps t = a' s + b (alias row a = group * SA + a', alias column b; s = N1 / n2) at (u + n2 a,
+    // v + n2 b) of the N1 x N1 filter, four consecutive taps per 16-byte load.
     plan->o2r.assign(J, 0);
     std::vector<float> psil;
-    std::vector<long long> psil_off(static_cast<size_t>(J) * L, -1);
+    std::vector<long long> psil_off(static_cast<size_t>(J) * J * L, -1);
     {
         bool o2r_on = true;
         if (const char* e = diag_env("WST_O2R")) o2r_on = std::atoi(e) != 0;
         const FamilyOps* fops = family_ops(plan->fam_m, plan->fam_n);
         for (int j1 = 0; j1 + 1 < J && o2r_on && max_order >= 2; ++j1) {
             const int n1 = g.PM >> j1;
-            if (g.PM != g.PN || plan->fam_m != plan->fam_n || !fops || !wstdev::o2r_size(n1) ||
-                g.oM != 4 || g.oN != 4 || oms != 4 || std::max(g.PM, g.PN) >> j1 > wstbig::kBigMinN ||
-                j1 >= wst::psi_levels(j1 + 1, J))
-                continue;
+            bool ok = g.PM == g.PN && plan->fam_m == plan->fam_n && fops && wstdev::o2r_size(n1) &&
+                      g.oM == 4 && g.oN == 4 && oms == 4 && std::max(g.PM, g.PN) >> j1 <= wstbig::kBigMinN;
+            for (int d = 1; ok && d <= wstdev::o2r_depth(n1) && j1 + d < J; ++d)
+                ok = j1 < wst::psi_levels(j1 + d, J);
+            if (!ok) continue;
             plan->o2r[j1] = 1;
-            const int n2 = n1 / 2, R = n2 / 8;
-            for (int l2 = 0; l2 < L; ++l2) {
-                psil_off[static_cast<size_t>(j1) * L + l2] = static_cast<long long>(psil.size());
-                const auto& f = fb.psi[static_cast<size_t>(j1 + 1) * L + l2][j1];
-                for (int i = 0; i < R; ++i)
-                    for (int k = 0; k < R; ++k)
-                        for (int lane = 0; lane < 64; ++lane) {
-                            const int u = 8 * i + wstdev::rev3(wstdev::o2r_h(lane));
-                            const int v = 8 * k + wstdev::rev3(wstdev::o2r_g(lane));
-                            psil.push_back(static_cast<float>(f[static_cast<size_t>(u) * n1 + v]));
-                            psil.push_back(static_cast<float>(f[static_cast<size_t>(u) * n1 + v + n2]));
-                            psil.push_back(static_cast<float>(f[static_cast<size_t>(u + n2) * n1 + v]));
-                            psil.push_back(static_cast<float>(f[static_cast<size_t>(u + n2) * n1 + v + n2]));
-                        }
+            for (int d = 1; d <= wstdev::o2r_depth(n1) && j1 + d < J; ++d) {
+                const int j2 = j1 + d, n2 = n1 >> d, G = wstdev::o2r_grid(n2), R = n2 / G, s = n1 / n2;
+                const int NG = G == 4 ? 4 : 1, SA = s / NG, T = SA * s;
+                for (int l2 = 0; l2 < L; ++l2) {
+                    psil_off[(static_cast<size_t>(j1) * J + j2) * L + l2] = static_cast<long long>(psil.size());
+                    const auto& f = fb.psi[static_cast<size_t>(j2) * L + l2][j1];
+                    const size_t base = psil.size();
+                    psil.resize(base + static_cast<size_t>(R) * R * T * 64);
+                    for (int lane = 0; lane < 64; ++lane) {
+                        const int r0 = wstdev::o2r_rev(wstdev::o2r_h(lane, G), G);
+                        const int c0 = wstdev::o2r_rev(wstdev::o2r_g(lane, G), G);
+                        const int ag = NG > 1 ? lane >> 4 : 0;
+                        for (int i = 0; i < R; ++i)
+                            for (int k = 0; k < R; ++k)
+                                for (int t = 0; t < T; ++t) {
+                                    const int e = i * R + k, a = ag * SA + t / s, b = t % s;
+                                    const int u = G * i + r0 + n2 * a, v = G * k + c0 + n2 * b;
+                                    psil[base + ((static_cast<size_t>(e) * (T / 4) + t / 4) * 64 + lane) * 4 + t % 4] =
+                                        static_cast<float>(f[static_cast<size_t>(u) * n1 + v]);
+                                }
+                    }
+                }
             }
         }
     }
@@ -1071,7 +1081,7 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
                             plan->dp, j1, nimg, img0, hexp, d_out, pooled))
             return fail(WST_ERR_UNSUPPORTED, "k_o2r not compiled for level size " + std::to_string(n1));
         WST_HIP_CHECK(hipGetLastError());
-        j2first = j1 + 2;
+        j2first = j1 + 1 + wstdev::o2r_depth(n1);
         if (j2first >= g.J) return timer.end(stream, 1 + g.J + j1);
     }
     if (plan->o2_export[j1]) {   // spectrum exported fully transformed: fold from HBM

@@ -24,6 +24,80 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return start, start + base + (1 if rank < rem else 0)
 
 
+class ShardGather:
+    """All-gather of per-rank shards into preallocated buffers (SURVEY.md §8(e) exchange step).
+
+    ``local`` holds this rank's shard (rows = its patches, ``shard_range`` order), padded to the
+    largest shard, so compute writes straight into it and one ``all_gather_into_tensor`` (one RCCL
+    call; ``all_gather`` of chunks under gloo) moves every shard with no staging copy.  ``gather``
+    returns the ``(n_total, ...)`` result: a view of the receive buffer when the shards are equal
+    (n_total % world == 0, e.g. BASELINE c3's 10^6 patches over 1/2/4/8 GPUs), else a compacted
+    copy.  ``to_root`` gathers to rank ``root`` only (the others receive nothing).  Buffers are
+    allocated once, outside any timed region."""
+
+    def __init__(self, n_total: int, row_shape, dtype, device, group=None, root_only: bool = False):
+        import torch
+        import torch.distributed as dist
+
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.n_total = n_total
+        self.lo, self.hi = shard_range(n_total, self.rank, self.world)
+        self.cap = shard_range(n_total, 0, self.world)[1]     # rank 0 holds the largest shard
+        self.root_only = root_only
+        row_shape = tuple(row_shape)
+        self.local = torch.zeros((self.cap,) + row_shape, dtype=dtype, device=device)
+        self.full = None
+        if self.world > 1 and (not root_only or self.rank == 0):
+            self.full = torch.empty((self.world * self.cap,) + row_shape, dtype=dtype, device=device)
+        self.equal = n_total % self.world == 0
+
+    @property
+    def mine(self) -> int:
+        return self.hi - self.lo
+
+    def bytes_moved(self) -> int:
+        """Payload bytes of one gather (all shards, padding included)."""
+        return 0 if self.world == 1 else self.world * self.local.numel() * self.local.element_size()
+
+    def gather(self):
+        import torch
+        import torch.distributed as dist
+
+        if self.world == 1:
+            return self.local[: self.mine]
+        gloo = dist.get_backend(self.group) == "gloo"
+        if self.root_only:
+            parts = list(self.full.chunk(self.world)) if self.rank == 0 else None
+            dist.gather(self.local, parts, dst=0, group=self.group)
+            if self.rank != 0:
+                return None
+        elif gloo:
+            dist.all_gather(list(self.full.chunk(self.world)), self.local, group=self.group)
+        else:
+            dist.all_gather_into_tensor(self.full, self.local, group=self.group)
+        if self.equal:
+            return self.full
+        keep = []
+        for r in range(self.world):
+            a, b = shard_range(self.n_total, r, self.world)
+            keep.append(self.full[r * self.cap: r * self.cap + (b - a)])
+        return torch.cat(keep, 0)
+
+
+def run_sharded_job(sg: "ShardGather", batch: int, generate: Callable, compute: Callable, gather: bool = True):
+    """One pass of a patch-sharded job (BASELINE c3; bench.py --config c3 runs exactly this): this
+    rank's patches [lo, hi) in batches of ``batch``, ``generate(first_global_index, n)`` makes them
+    (keyed by global index, so no rank needs another's inputs), ``compute(x, n, out_rows)`` writes
+    their outputs into this rank's rows of ``sg.local``; then the all-gather (when ``gather``)."""
+    for b0 in range(0, sg.mine, batch):
+        nb = min(batch, sg.mine - b0)
+        x = generate(sg.lo + b0, nb)
+        compute(x, nb, sg.local[b0: b0 + nb])
+    return sg.gather() if gather else sg.local[: sg.mine]
+
+
 def gather_shards(local, n_total: int, group=None):
     """All-gather per-rank shards (first dim = this rank's patches, ranges from ``shard_range``)
     into the full ``(n_total, ...)`` tensor on every rank.  Shards are padded to the largest shard
