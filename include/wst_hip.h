@@ -71,7 +71,8 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
 typedef struct wst_filter_convention {
     double norm_pi;
     int periodize_half;   /* 0..8 */
-    int reserved;         /* 0 */
+    int flags;            /* bit 0: gabor_2d's rotation matrices R, R_inv in float32 (default 0:
+                             float64); other bits 0 */
 } wst_filter_convention;
 
 int wst_default_convention(wst_filter_convention* out);

@@ -64,10 +64,15 @@ class FilterConvention:
     periodize_half  the periodisation grid ex, ey in [-h, h] (5x5 copies for h = 2).
     gabor_dtype     accumulator of gabor_2d (complex128; complex64 in versions that allocate
                     ``np.zeros((M, N), np.complex64)``).  Oracle-only switch: the device filters
-                    are float32 either way (tests/test_convention.py measures its effect)."""
+                    are float32 either way (tests/test_convention.py measures its effect).
+    rot_dtype       dtype of gabor_2d's rotation matrices R, R_inv (float64; versions that write
+                    ``np.array(..., np.float32)`` round cos/sin of theta to float32 in the
+                    envelope's curvature, not in the modulation).  Shared with the library
+                    (wst_filter_convention flags bit 0)."""
     norm_pi: float = 3.1415
     periodize_half: int = 2
     gabor_dtype: type = np.complex128
+    rot_dtype: type = np.float64
 
 
 KYMATIO_0_3_0 = FilterConvention()
@@ -117,8 +122,8 @@ def gabor_2d(M, N, sigma, theta, xi, slant=1.0, offset=0, conv=KYMATIO_0_3_0):
     ``xx`` runs along axis 0 on the asymmetric grid [ex*M, ex*M + M).  ``conv`` holds the
     recalled constants (FilterConvention)."""
     gab = np.zeros((M, N), conv.gabor_dtype)
-    R = np.array([[np.cos(theta), -np.sin(theta)], [np.sin(theta), np.cos(theta)]], np.float64)
-    R_inv = np.array([[np.cos(theta), np.sin(theta)], [-np.sin(theta), np.cos(theta)]], np.float64)
+    R = np.array([[np.cos(theta), -np.sin(theta)], [np.sin(theta), np.cos(theta)]], conv.rot_dtype)
+    R_inv = np.array([[np.cos(theta), np.sin(theta)], [-np.sin(theta), np.cos(theta)]], conv.rot_dtype)
     D = np.array([[1, 0], [0, slant * slant]])
     curv = np.dot(R, np.dot(D, R_inv)) / (2 * sigma * sigma)
     h = conv.periodize_half

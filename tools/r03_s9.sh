@@ -1,0 +1,14 @@
+#!/bin/bash
+# parity + k_o12 timing A/B (dev): tools/r03_s9.sh <tag>
+tag=$1
+cd "$GRAFT_REPO_ROOT" || exit 99
+mkdir -p gpurun_out/$tag
+tools/gpu_step.sh 600 gpurun_out/$tag/pytest.txt python3 -u -m pytest tests -m gpu -q -rs -x --timeout 120 --timeout-method thread || exit 99
+tail -3 gpurun_out/$tag/pytest.txt
+for lib in libwst_hip.so var_t768.so; do
+  WST_LIB=$lib timeout -k 10 200 python3 tools/kernel_ms.py 1536 2048 > gpurun_out/$tag/kms_$lib.txt 2>&1 || exit 99
+  cat gpurun_out/$tag/kms_$lib.txt | grep chunk
+done
+WST_LIB=var_nofuse.so WST_O12=0 timeout -k 10 200 python3 tools/kernel_ms.py 1536 > gpurun_out/$tag/kms_nofuse.txt 2>&1 || exit 99
+grep chunk gpurun_out/$tag/kms_nofuse.txt
+bash tools/ab_kernel.sh $tag "k_o12|k_o2<|k_o1<3, 3, 136" libwst_hip.so

@@ -38,17 +38,20 @@ class Convention(ctypes.Structure):
     """``wst_filter_convention`` (include/wst_hip.h): the recalled kymatio constants, mirrored by
     ``oracle.kymatio_ref.FilterConvention``.  Defaults = kymatio 0.3.0 (3.1415, 5x5 grid)."""
     _fields_ = [("norm_pi", ctypes.c_double), ("periodize_half", ctypes.c_int),
-                ("reserved", ctypes.c_int)]
+                ("flags", ctypes.c_int)]
 
-    def __init__(self, norm_pi=3.1415, periodize_half=2):
-        super().__init__(float(norm_pi), int(periodize_half), 0)
+    def __init__(self, norm_pi=3.1415, periodize_half=2, rot_f32=False, flags=None):
+        super().__init__(float(norm_pi), int(periodize_half),
+                         int(flags) if flags is not None else (1 if rot_f32 else 0))
 
 
 def _conv_ptr(convention):
     if convention is None:
         return None
     if not isinstance(convention, Convention):   # anything with the two fields (oracle's class)
-        convention = Convention(convention.norm_pi, convention.periodize_half)
+        import numpy as _np
+        rot32 = getattr(convention, "rot_dtype", _np.float64) == _np.float32
+        convention = Convention(convention.norm_pi, convention.periodize_half, rot_f32=rot32)
     return ctypes.byref(convention)
 
 

@@ -92,7 +92,12 @@ void fft2(std::vector<cdouble>& a, int rows, int cols, int sign) {
 std::vector<cdouble> gabor_2d(int M, int N, double sigma, double theta, double xi, double slant,
                               const FilterConvention& conv) {
     std::vector<cdouble> gab(static_cast<size_t>(M) * N, cdouble(0.0, 0.0));
-    const double c = std::cos(theta), s = std::sin(theta);
+    double c = std::cos(theta), s = std::sin(theta);
+    const double cx = c * xi, sy = s * xi;   // the modulation uses cos / sin of theta unrounded
+    if (conv.rot_f32) {                      // R, R_inv stored as float32 (convention flag)
+        c = static_cast<double>(static_cast<float>(c));
+        s = static_cast<double>(static_cast<float>(s));
+    }
     // curv = R diag(1, slant^2) R^-1 / (2 sigma^2),  R = [[c, -s], [s, c]]
     const double d1 = 1.0, d2 = slant * slant;
     const double inv = 1.0 / (2.0 * sigma * sigma);
@@ -100,7 +105,6 @@ std::vector<cdouble> gabor_2d(int M, int N, double sigma, double theta, double x
     const double c01 = (c * s * d1 - s * c * d2) * inv;
     const double c10 = (s * c * d1 - c * s * d2) * inv;
     const double c11 = (s * s * d1 + c * c * d2) * inv;
-    const double cx = c * xi, sy = s * xi;
     const int h = conv.periodize_half;
     for (int ex = -h; ex <= h; ++ex) {
         for (int ey = -h; ey <= h; ++ey) {

@@ -21,8 +21,9 @@ using cdouble = std::complex<double>;
 struct FilterConvention {
     double norm_pi = 3.1415;   // "pi" of gabor_2d's normaliser 2*pi*sigma^2/slant (literal 3.1415)
     int periodize_half = 2;    // periodisation copies ex, ey in [-h, h] (5x5 grid)
+    bool rot_f32 = false;      // rotation matrices R, R_inv of the envelope rounded to float32
 };
-constexpr FilterConvention kKymatio030{3.1415, 2};
+constexpr FilterConvention kKymatio030{3.1415, 2, false};
 
 struct Geometry {
     int M = 0, N = 0;     // input plane

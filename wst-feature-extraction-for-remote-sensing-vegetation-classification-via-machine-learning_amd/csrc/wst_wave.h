@@ -72,7 +72,7 @@ __host__ __device__ constexpr int o2r_lds(int n1c) {
 }
 // filter taps per element and lane of a path level: s^2 / (alias groups)
 __host__ __device__ constexpr int o2r_taps(int n1c, int n2) {
-    return (n1c / n2) * (n1c / n2) / (o2r_grid(n2) == 4 ? 4 : 1);
+    return o2r_grid(n2) == 4 ? 4 : (n1c / n2) * (n1c / n2);   // 4 x 4 grids: the windowed fold
 }
 constexpr int kO2rWaves = 8;   // waves per workgroup: one theta2 each
 #ifndef WST_O2R_AHEAD
@@ -273,13 +273,13 @@ __device__ __forceinline__ void o2r_emit(float v, int idx0, int lane, long long 
 // N1C: level j1 size; N2: path level size.  Hs: the half spectrum in LDS (row stride S, row N1C =
 // row 0); fl: the path's lane-ordered filter taps; tw2 / GM / GN: the path level's tables in LDS.
 template <int N1C, int N2>
-__device__ __forceinline__ void o2r_path(const float2* Hs, const float* __restrict__ fl, const float2* tw2,
-                                         const float* GM, const float* GN, int lane, long long img, int K,
-                                         int k0, float* __restrict__ out, int pooled) {
+__device__ __forceinline__ void o2r_path(const float2* Hs, const float* __restrict__ fl, int win,
+                                         const float2* tw2, const float* GM, const float* GN, int lane,
+                                         long long img, int K, int k0, float* __restrict__ out, int pooled) {
     constexpr int G = o2r_grid(N2), R = N2 / G, S = o2r_stride(N1C), SS = N1C / N2;
     constexpr int NG = G == 4 ? 4 : 1;          // alias groups (lane bits 4, 5 when G = 4)
-    constexpr int SA = SS / NG;                 // alias rows per group
-    constexpr int T = SA * SS, T4 = T / 4;      // filter taps per element, float4 loads per element
+    constexpr int SA = SS / NG;                 // alias rows per group (dense fold)
+    constexpr int T = G == 4 ? 4 : SA * SS, T4 = T / 4;   // filter taps per element, float4 loads
     static_assert(T % 4 == 0 && R * G == N2, "k_o2r level");
     const int g = o2r_g(lane, G), h = o2r_h(lane, G);
     const int c0 = o2r_rev(g, G), r0 = o2r_rev(h, G);
@@ -300,6 +300,51 @@ __device__ __forceinline__ void o2r_path(const float2* Hs, const float* __restri
         wstfft::static_for<0, R * R>([&](auto ec) {
             constexpr int e = decltype(ec)::value;
             v[e / R][e % R] = qd[e * 8];
+        });
+    } else if constexpr (G == 4) {
+        // windowed fold (the 12 x 12 paths: s = 4 or 8, filters compact): the filter's significant
+        // bins lie in a window of 4 x 4 alias tiles starting at tile (alpha, beta) (host: psil_win;
+        // a band of width n2 in each direction at most 3 tiles long, plus the offset within a tile).
+        // Lane group ag takes alias row rho = alpha + ag, every lane the 4 alias columns
+        // kappa_j = beta + j (mod s); whether column kappa_j is read direct or as the conjugate
+        // mirror is wave-uniform.
+        const int alpha = win & 255, beta = win >> 8;
+        const int rho = (alpha + ag) & (SS - 1);
+        int wd = (r0 + N2 * rho) * S + c0;
+        int wm = (N1C - r0 - N2 * rho - G * (R - 1)) * S + (N1C - c0 - G * (R - 1));
+        float4 f[R * R];
+        wstfft::static_for<0, R * R>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            f[e] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, e * 1024, 0));
+        });
+        wstfft::static_for<0, R * R>([&](auto ec) { v[decltype(ec)::value / R][decltype(ec)::value % R] = make_float2(0.f, 0.f); });
+        wstfft::static_for<0, 4>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            const int kappa = (beta + j) & (SS - 1);
+            float2 hv[R * R];
+            float sg;
+            if (2 * kappa < SS) {
+                const float2* q = Hs + (wd + N2 * kappa);
+                wstfft::static_for<0, R * R>([&](auto ec) {
+                    constexpr int e = decltype(ec)::value;
+                    hv[e] = q[G * (e / R) * S + G * (e % R)];
+                });
+                sg = 1.f;
+            } else {
+                const float2* q = Hs + (wm - N2 * kappa);
+                wstfft::static_for<0, R * R>([&](auto ec) {
+                    constexpr int e = decltype(ec)::value;
+                    hv[e] = q[G * (R - 1 - e / R) * S + G * (R - 1 - e % R)];
+                });
+                sg = -1.f;
+            }
+            wstfft::static_for<0, R * R>([&](auto ec) {
+                constexpr int e = decltype(ec)::value;
+                const float fj = j == 0 ? f[e].x : j == 1 ? f[e].y : j == 2 ? f[e].z : f[e].w;
+                float2& a = v[e / R][e % R];
+                a.x = fmaf(hv[e].x, fj, a.x);
+                a.y = fmaf(sg * hv[e].y, fj, a.y);
+            });
         });
     } else {
         // fold, software-pipelined over the steps (element e, tap quad t4): the taps of step
@@ -446,9 +491,14 @@ __device__ __forceinline__ void o2r_path(const float2* Hs, const float* __restri
 // ---------------------------------------------------------------------------------------------
 // One workgroup of 8 waves per (plane, theta1) at level j1 (N1C x N1C, square family FAM); 4 x 4
 // output maps.  hexp: k_o1's half spectra (rows transformed, digit-reversed row order).
+// nwl: path levels j1 + 1 .. j1 + nwl run wave-resident; when nwl < DEPTH the workgroup then
+// runs the remaining levels j1 + nwl + 1 .. J - 1 through k_o2_body's LDS batches (layout lay2:
+// the same spectrum at row stride S, a B region of its own) after one barrier -- the hybrid
+// measured fastest at c2 (the wave form's dense s = 4 / 8 folds read 4x the filter bytes of
+// the box-sparse batch folds).
 template <int FAM, int N1C>
-__global__ void __launch_bounds__(64 * kO2rWaves, 4) k_o2r(DevParams p, int j1, int nimg, long long img0,
-                                                          const float2* __restrict__ hexp,
+__global__ void __launch_bounds__(64 * kO2rWaves, 4) k_o2r(DevParams p, LdsLayout lay2, int nwl, int j1, int nimg,
+                                                          long long img0, const float2* __restrict__ hexp,
                                                           float* __restrict__ out, int pooled) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int HLD = N1C / 2 + 1, S = o2r_stride(N1C), DEPTH = o2r_depth(N1C);
@@ -511,20 +561,34 @@ __global__ void __launch_bounds__(64 * kO2rWaves, 4) k_o2r(DevParams p, int j1, 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
     const int kbase = p.o2_base[j1 * L + l1];
+    // waves 4..7 take the levels in a rotated order (2, 3, 1): the two halves of the workgroup
+    // are then in different phases (L2-bound folds beside VALU-bound transforms) instead of
+    // reaching the same phase together
+#ifndef WST_O2R_ROT
+#define WST_O2R_ROT 1
+#endif
+    const int rot = WST_O2R_ROT && (wave >= kO2rWaves / 2) && nwl > 1 ? 1 : 0;
     for (int l2 = (WST_O2R_SKIP & 1) ? L : wave; l2 < L; l2 += kO2rWaves) {
-        unsigned char* t = lvl;
-        wstfft::static_for<1, DEPTH + 1>([&](auto dc) {
-            constexpr int d = decltype(dc)::value;
-            constexpr int n2 = N1C >> d;
-            const int j2 = j1 + d;
-            const float2* tw2 = reinterpret_cast<const float2*>(t);
-            const float* GM = reinterpret_cast<const float*>(tw2 + n2);
-            const float* GN = GM + n2 * 4;
-            if (j2 < J && ((WST_O2R_LEVELS >> (d - 1)) & 1))
-                o2r_path<N1C, n2>(H, p.psil + p.psil_off[(j1 * J + j2) * L + l2], tw2, GM, GN, lane, img,
-                                  p.K, kbase + (d - 1) * L + l2, out, pooled);
-            t += n2 * (8 + 32);
-        });
+#pragma unroll 1
+        for (int step = 0; step < nwl; ++step) {
+            const int d = (step + rot) % nwl + 1;
+            wstfft::static_for<1, DEPTH + 1>([&](auto dc) {
+                constexpr int dd = decltype(dc)::value;
+                constexpr int n2 = N1C >> dd;
+                const int j2 = j1 + dd;
+                const float2* tw2 = reinterpret_cast<const float2*>(lvl + o2r_level_bytes(N1C, dd - 1));
+                const float* GM = reinterpret_cast<const float*>(tw2 + n2);
+                const float* GN = GM + n2 * 4;
+                const int pi = (j1 * J + j2) * L + l2;
+                if (d == dd && j2 < J && ((WST_O2R_LEVELS >> (dd - 1)) & 1))
+                    o2r_path<N1C, n2>(H, p.psil + p.psil_off[pi], p.psil_win[pi], tw2, GM, GN, lane, img,
+                                      p.K, kbase + (dd - 1) * L + l2, out, pooled);
+            });
+        }
+    }
+    if (nwl < DEPTH && j1 + nwl + 1 < J) {
+        __syncthreads();   // every wave done with this kernel's tables (B reuses their LDS)
+        k_o2_body<FAM, FAM, CAP, 1, 0, 4, true>(smem, p, lay2, j1, nimg, img0, nullptr, out, pooled, j1 + nwl + 1, S);
     }
 }
 
