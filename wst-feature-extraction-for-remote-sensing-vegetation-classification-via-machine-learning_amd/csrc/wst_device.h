@@ -90,14 +90,6 @@ struct DevParams {
     const float* lpw;
     const int* lpw_off;
     int oMp, oNp;
-    // k_o2r (wst_wave.h): the order-2 filters of level j2 = j1 + 1 in the kernel's lane order
-    // (per path: R x R elements x 64 lanes x 4 alias taps, floats; [j1 * L + l2], -1 = not built)
-    // and the natural-order tap matrices ([2r] GM_r, [2r + 1] GN_r; rows of 4 floats)
-    const float* psil;
-    const long long* psil_off;
-    const int* psil_win;          // 4 x 4-grid levels: alias-tile window start alpha | beta << 8
-    const float* lpn;
-    const int* lpn_off;
 };
 
 // Per-launch LDS layout (byte offsets) and the table slices copied into LDS.
@@ -1387,7 +1379,7 @@ constexpr int o1_min_waves(int cap, int fm, int fn) {
 // k_o1: one workgroup per (plane, theta1) at fixed j1 -- order 1 + half-spectrum export
 // ------------------------------------------------------------------------------------------
 // k_o1 body; OC > 0: the output maps are OC x OC (compile-time; the common 4 x 4 of the headline)
-template <int FM, int FN, int MAXN, int SQ, int OC, bool FUSE = false>
+template <int FM, int FN, int MAXN, int SQ, int OC>
 __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& p,
                                           const LdsLayout& lay, int j1, int nimg, long long img0,
                                           const float2* __restrict__ xhat, float2* __restrict__ hexp,
@@ -1455,8 +1447,8 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
 
     // 5. split into the two rows' half spectra (columns 0..nN1/2) and export them
     const int hld = (nN1 >> 1) + 1;
-    float2* H = FUSE ? nullptr : hexp + static_cast<long long>(item) * nM1 * hld;
-    if (FUSE || lay.export_full) {
+    float2* H = hexp + static_cast<long long>(item) * nM1 * hld;
+    if (lay.export_full) {
         // in place: packed row 2t -> half-spectrum rows 2t and 2t+1 (the odd rows of A are free),
         // then the column FFTs (rows digit-reversed -> natural); k_o2 folds the fully transformed
         // spectrum from HBM/L2 and keeps only its path batches in LDS (host: nh * hld <= KS * T)
@@ -1489,29 +1481,6 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
         __syncthreads();
         lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(A, wstfft::Lines{1, 0, hld, 1, ld1}, nM1,
                                                                      tb.twM(j1), id);
-        if constexpr (FUSE) {
-            // k_o12: the order-2 part follows in this workgroup -- compact the spectrum in LDS to
-            // row stride hld at offset 0 (read everything first: source and target overlap)
-            constexpr int KC = 12;
-            const int nitems2 = nM1 * hld;
-            float2 c[KC];
-#pragma unroll
-            for (int k = 0; k < KC; ++k) {
-                const int w = threadIdx.x + k * T;
-                if (w < nitems2) {
-                    const int r = dh.div(w);
-                    c[k] = A[r * ld1 + (w - r * hld)];
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < KC; ++k) {
-                const int w = threadIdx.x + k * T;
-                if (w < nitems2) A[w] = c[k];
-            }
-            __syncthreads();
-            return;
-        }
         for (GridIter it(hld); it.u < nM1; it.next()) stnt(H + it.u * hld + it.v, A[it.u * ld1 + it.v]);
         return;
     }
@@ -1557,11 +1526,11 @@ constexpr int o2_min_waves(int cap) { return cap == 48 ? 6 : cap == 24 ? 5 : 1; 
 #ifndef WST_HG_R
 #define WST_HG_R (HG ? 2 : 1)
 #endif
-template <int FM, int FN, int MAXN, int SQ, int HG, int OC, bool FUSE = false>
+template <int FM, int FN, int MAXN, int SQ, int HG, int OC>
 __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& p,
                                           const LdsLayout& lay, int j1, int nimg, long long img0,
                                           const float2* __restrict__ hexp, float* __restrict__ out,
-                                          int pooled, int j2first, int hs_fuse = 0) {
+                                          int pooled, int j2first) {
     const int oM = OC ? OC : p.oM, oN = OC ? OC : p.oN;
     const int oms = OC ? 4 : lay.oms;
     const int J = p.J, L = p.L;
@@ -1606,7 +1575,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     // big level
     constexpr int PHI = (SQ && !HG) ? MAXN / 2 : MAXN;
 
-    if constexpr (!HG && !FUSE) {
+    if constexpr (!HG) {
         // 1. half spectrum rows -> LDS, then the column FFTs (rows digit-reversed -> natural)
         float2* Hl = reinterpret_cast<float2*>(smem);
         if (!(dbg & 1024)) copy_to_lds(Hl, Hg, nM1 * hld);
@@ -1615,7 +1584,6 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(
                 Hl, wstfft::Lines{1, 0, hld, 1, hld}, nM1, tb.twM(j1), id);
     }
-    if constexpr (FUSE) __syncthreads();   // this body's tables in place before any reads them
     WST_STAMP(sctr);
 
     // 2. order-2 paths in batches: Hermitian fold -> |ifft| -> S2 low-pass
@@ -1640,8 +1608,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             const long long pstride = static_cast<long long>(n1);
             const int* bx = p.box + p.box_off[j2 * J + j1] + (l2a >> 1) * (nM2 + nN2);
             if (!(dbg & 8) && !(dbg & (s2 == 2 ? 256 : 512)))
-                fold2_any<WST_HG_R>(s2, H, FUSE ? hs_fuse : hld, nM1, nN1, ps, pstride, npair, npath, B, pslot,
-                                    ld2, nM2, nN2,
+                fold2_any<WST_HG_R>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
                           bx, nM2 + nN2);
             __syncthreads();
             WST_STAMP(sctr);
@@ -1722,32 +1689,6 @@ __global__ void __launch_bounds__((HG && !SQ) ? WST_O2X_BOUND : 1024, o2_min_wav
         }
     }
     k_o2_body<FM, FN, MAXN, SQ, HG, 0>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
-}
-
-// ------------------------------------------------------------------------------------------
-// k_o12: k_o1 and k_o2 of one LDS-resident level j1 fused -- one workgroup per (plane, theta1)
-// computes U1, S1 and the U1 spectrum (k_o1_body, in-place Hermitian split and column FFTs), keeps
-// the spectrum in LDS (compacted to row stride nN1 / 2 + 1) and runs every order-2 path from it
-// (k_o2_body).  Removes the HBM hand-off of the half spectra (c2: 301 KB per plane written by
-// k_o1 and read back by k_o2) and k_o2's copy-in and column FFTs.  lay1 / lay2: the two bodies'
-// LDS layouts (lay1.export_full = 1); the launch takes max of their sizes.
-// ------------------------------------------------------------------------------------------
-template <int FM, int FN, int MAXN, int SQ>
-__global__ void __launch_bounds__(1024) k_o12(DevParams p, LdsLayout lay1, LdsLayout lay2, int j1,
-                                              int nimg, long long img0, const float2* __restrict__ xhat,
-                                              float* __restrict__ out, int pooled) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    if constexpr (SQ && MAXN == 136) {
-        if (p.oM == 4 && p.oN == 4 && lay1.oms == 4 && lay2.oms == 4) {
-            k_o1_body<FM, FN, MAXN, SQ, 4, true>(smem, p, lay1, j1, nimg, img0, xhat, nullptr, out, pooled);
-            k_o2_body<FM, FN, MAXN, SQ, 0, 4, true>(smem, p, lay2, j1, nimg, img0, nullptr, out, pooled, j1 + 1,
-                                                    (p.PN >> (j1 + 1)) + 1);
-            return;
-        }
-    }
-    k_o1_body<FM, FN, MAXN, SQ, 0, true>(smem, p, lay1, j1, nimg, img0, xhat, nullptr, out, pooled);
-    k_o2_body<FM, FN, MAXN, SQ, 0, 0, true>(smem, p, lay2, j1, nimg, img0, nullptr, out, pooled, j1 + 1,
-                                            (p.PN >> (j1 + 1)) + 1);
 }
 
 }  // namespace wstdev

@@ -23,7 +23,6 @@
 #include "filter_bank.h"
 #include "wst_hip.h"
 #include "wst_launch.h"
-#include "wst_wave.h"
 
 using wstdev::DevParams;
 using wstdev::LdsLayout;
@@ -156,17 +155,6 @@ struct wst_plan {
     std::vector<int> box_off_host;
     float* d_lpt = nullptr;
     int* d_lpt_off = nullptr;
-    float* d_psil = nullptr;          // k_o2r lane-ordered order-2 filters (wst_wave.h)
-    long long* d_psil_off = nullptr;
-    int* d_psil_win = nullptr;
-    int* d_lpn_off = nullptr;
-    std::vector<int> o2r;             // per j1: k_o2r runs the order-2 paths (first o2r_nwl levels
-    std::vector<int> o2r_nwl;         //   wave-resident, the rest through k_o2_body's batches)
-    std::vector<LdsLayout> o2r_lay2;
-    std::vector<size_t> o2r_lds;
-    std::vector<int> o12;             // per j1: k_o1 + k_o2 fused (k_o12), spectrum kept in LDS
-    std::vector<int> o12_threads;
-    std::vector<size_t> o12_lds;
     // launch geometry
     int fam_m = 0, fam_n = 0;   // FFT size families (odd part of PM / PN), 0 = generic DFT
     const FamilyOps* ops = nullptr;
@@ -237,10 +225,6 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_lpn);
     (void)hipFree(p->d_lpw);
     (void)hipFree(p->d_lpw_off);
-    (void)hipFree(p->d_psil);
-    (void)hipFree(p->d_psil_off);
-    (void)hipFree(p->d_psil_win);
-    (void)hipFree(p->d_lpn_off);
     for (auto& kv : p->ws_by_stream)
         if (kv.second.ptr) (void)hipFree(kv.second.ptr);
     delete p;
@@ -586,90 +570,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                     lpn.push_back(a < no ? static_cast<float>(h[((sdec * (a + 1) - p) % n + n) % n]) : 0.f);
         }
     plan->oms = oms;
-    // k_o2r (wst_wave.h): square compiled levels N1 (96 / 48) of a plane with 4 x 4 maps, every
-    // order-2 path j2 = j1 + d (d = 1 .. o2r_depth, n2 = N1 >> d) held in one wave.  Per path
-    // (j2, l2) the filter psi_{j2, l2} at level j1 in the kernel's lane order: element (i, k) of lane
-    // (h, g) of the G x G grid is bin (u, v) = (G i + rev(h), G k + rev(g)) of the n2 x n2 fold, its
-    // taps t = a' s + b (alias row a = group * SA + a', alias column b; s = N1 / n2) at (u + n2 a,
-    // v + n2 b) of the N1 x N1 filter, four consecutive taps per 16-byte load.
-    plan->o2r.assign(J, 0);
-    std::vector<float> psil;
-    std::vector<long long> psil_off(static_cast<size_t>(J) * J * L, -1);
-    std::vector<int> psil_win(static_cast<size_t>(J) * J * L, 0);
-    {
-        bool o2r_on = true;
-        if (const char* e = diag_env("WST_O2R")) o2r_on = std::atoi(e) != 0;
-        const FamilyOps* fops = family_ops(plan->fam_m, plan->fam_n);
-        for (int j1 = 0; j1 + 1 < J && o2r_on && max_order >= 2; ++j1) {
-            const int n1 = g.PM >> j1;
-            bool ok = g.PM == g.PN && plan->fam_m == plan->fam_n && fops && wstdev::o2r_size(n1) &&
-                      g.oM == 4 && g.oN == 4 && oms == 4 && std::max(g.PM, g.PN) >> j1 <= wstbig::kBigMinN;
-            for (int d = 1; ok && d <= wstdev::o2r_depth(n1) && j1 + d < J; ++d)
-                ok = j1 < wst::psi_levels(j1 + d, J);
-            // 4 x 4-grid levels fold a window of 4 x 4 alias tiles: every significant bin (above
-            // kBoxThreshold of the filter's maximum, the box folds' criterion) must lie in it
-            std::vector<int> wins(static_cast<size_t>(J) * L, 0);
-            for (int d = 1; ok && d <= wstdev::o2r_depth(n1) && j1 + d < J; ++d) {
-                const int n2 = n1 >> d, sa = n1 / n2;
-                if (wstdev::o2r_grid(n2) != 4) continue;
-                for (int l2 = 0; ok && l2 < L; ++l2) {
-                    const auto& f = fb.psi[static_cast<size_t>(j1 + d) * L + l2][j1];
-                    double mx = 0.0;
-                    for (double x : f) mx = std::max(mx, std::fabs(x));
-                    std::vector<char> ra(sa, 0), ca(sa, 0);
-                    for (int r = 0; r < n1; ++r)
-                        for (int c = 0; c < n1; ++c)
-                            if (std::fabs(f[static_cast<size_t>(r) * n1 + c]) > kBoxThreshold * mx) {
-                                ra[r / n2] = 1;
-                                ca[c / n2] = 1;
-                            }
-                    auto start = [&](const std::vector<char>& hit) {
-                        for (int a0 = 0; a0 < sa; ++a0) {
-                            bool cov = true;
-                            for (int a = 0; a < sa; ++a)
-                                if (hit[a] && ((a - a0 + sa) % sa) >= 4) cov = false;
-                            if (cov) return a0;
-                        }
-                        return -1;
-                    };
-                    const int al = start(ra), be = start(ca);
-                    if (al < 0 || be < 0) ok = false;
-                    else wins[static_cast<size_t>(j1 + d) * L + l2] = al | (be << 8);
-                }
-            }
-            if (!ok) continue;
-            plan->o2r[j1] = 1;
-            for (int d = 1; d <= wstdev::o2r_depth(n1) && j1 + d < J; ++d) {
-                const int j2 = j1 + d, n2 = n1 >> d, G = wstdev::o2r_grid(n2), R = n2 / G, s = n1 / n2;
-                const int NG = G == 4 ? 4 : 1, SA = s / NG, T = wstdev::o2r_taps(n1, n2);
-                for (int l2 = 0; l2 < L; ++l2) {
-                    psil_off[(static_cast<size_t>(j1) * J + j2) * L + l2] = static_cast<long long>(psil.size());
-                    const int win = wins[static_cast<size_t>(j2) * L + l2];
-                    psil_win[(static_cast<size_t>(j1) * J + j2) * L + l2] = win;
-                    const auto& f = fb.psi[static_cast<size_t>(j2) * L + l2][j1];
-                    const size_t base = psil.size();
-                    psil.resize(base + static_cast<size_t>(R) * R * T * 64);
-                    for (int lane = 0; lane < 64; ++lane) {
-                        const int r0 = wstdev::o2r_rev(wstdev::o2r_h(lane, G), G);
-                        const int c0 = wstdev::o2r_rev(wstdev::o2r_g(lane, G), G);
-                        const int ag = NG > 1 ? lane >> 4 : 0;
-                        for (int i = 0; i < R; ++i)
-                            for (int k = 0; k < R; ++k)
-                                for (int t = 0; t < T; ++t) {
-                                    const int e = i * R + k;
-                                    // dense: alias row ag SA + t / s, column t % s; windowed (4 x 4
-                                    // grids): row alpha + ag, column beta + t (mod s)
-                                    const int a = G == 4 ? ((win & 255) + ag) % s : ag * SA + t / s;
-                                    const int b = G == 4 ? ((win >> 8) + t) % s : t % s;
-                                    const int u = G * i + r0 + n2 * a, v = G * k + c0 + n2 * b;
-                                    psil[base + ((static_cast<size_t>(e) * (T / 4) + t / 4) * 64 + lane) * 4 + t % 4] =
-                                        static_cast<float>(f[static_cast<size_t>(u) * n1 + v]);
-                                }
-                    }
-                }
-            }
-        }
-    }
     // wide tap matrices for the MFMA low-pass (lds_lowpass_mfma), columns padded to x16:
     //   [2r + d] level r in physical order (r < J), [2J + d] level 0 in natural order (k_prep)
     const int oMp = (g.oM + 15) & ~15, oNp = (g.oN + 15) & ~15;
@@ -748,10 +648,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     if ((rc = upload(&plan->d_lpn, lpn)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_lpw, lpw)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_lpw_off, lpw_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_psil, psil)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_psil_off, psil_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_psil_win, psil_win)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_lpn_off, plan->lpn_off)) != WST_OK) return rc;
 
     DevParams& dp = plan->dp;
     dp.M = g.M; dp.N = g.N; dp.PM = g.PM; dp.PN = g.PN; dp.J = J; dp.L = L;
@@ -776,8 +672,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     if (const char* e = diag_env("WST_BOX1_MIN_S")) dp.box1_min_s = std::atoi(e);
     dp.lpt = plan->d_lpt; dp.lpt_off = plan->d_lpt_off;
     dp.lpw = plan->d_lpw; dp.lpw_off = plan->d_lpw_off; dp.oMp = oMp; dp.oNp = oNp;
-    dp.psil = plan->d_psil; dp.psil_off = plan->d_psil_off; dp.psil_win = plan->d_psil_win;
-    dp.lpn = plan->d_lpn; dp.lpn_off = plan->d_lpn_off;
     // square variant (bounded FFT sizes + fused order-2 low-pass): square plane of a compiled
     // family, oM <= kLpOM and every order-2 level's column units hold ceil(oM / 2) slots
     plan->sq = (plan->fam_m > 0 && plan->fam_m == plan->fam_n && g.PM == g.PN &&
@@ -1014,59 +908,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         plan->o2x_lay[j1].nsplit = 1;
         if (const char* e = diag_env("WST_O2X_SPLIT")) plan->o2x_lay[j1].nsplit = std::max(1, std::atoi(e));
     }
-    // k_o2r: the wave-resident first level, then the remaining levels through k_o2_body in the same
-    // workgroup from the same LDS spectrum (row stride o2r_stride, N1 + 1 rows), its batches of at
-    // most 4 paths in a B region after the spectrum (two workgroups per CU)
-    plan->o2r_nwl.assign(J, 0);
-    plan->o2r_lay2.assign(J, LdsLayout{});
-    plan->o2r_lds.assign(J, 0);
-    for (int j1 = plan->rb; j1 + 1 < J; ++j1) {
-        if (!plan->o2r[j1]) continue;
-        const int n1 = g.PM >> j1;
-        int nwl = 1;   // measured: every level wave-resident 1.22-1.27 ms per 1536 planes at c2 j1 = 0
-        if (const char* e = diag_env("WST_O2R_NWL")) nwl = std::max(1, std::min(std::atoi(e), wstdev::o2r_depth(n1)));
-        plan->o2r_nwl[j1] = nwl;
-        size_t lds = static_cast<size_t>(wstdev::o2r_lds(n1));
-        const int j2f = j1 + nwl + 1;
-        if (j2f < J) {
-            const size_t hbytes = static_cast<size_t>(n1 + 1) * wstdev::o2r_stride(n1) * sizeof(float2);
-            const size_t bcap = 4 * pslot(j2f);
-            size_t smax = 0;
-            for (int j2 = j2f; j2 < J; ++j2)
-                smax = std::max(smax, static_cast<size_t>(paths_per_batch(bcap, pslot(j2), L)) * omn);
-            const size_t l2 = layout(plan->o2r_lay2[j1], hbytes, bcap * sizeof(float2), t, Blocks{j1, J - 1, false},
-                                     1, 0, smax, Blocks{j1 + 1, J - 1, false}, oms);
-            lds = std::max(lds, l2);
-        }
-        plan->o2r_lds[j1] = lds;
-        if (lds > static_cast<size_t>(kMaxLds)) plan->o2r[j1] = 0;
-    }
-    // k_o12: square fused-low-pass levels with order-2 paths keep the U1 spectrum in LDS (k_o1 and
-    // k_o2 in one workgroup) when the in-place Hermitian split and the compaction fit their
-    // per-thread item budgets (8 and 12)
-    plan->o12.assign(J, 0);
-    plan->o12_threads.assign(J, 512);
-    plan->o12_lds.assign(J, 0);
-    {
-        // measured at c2 (per 1536 planes): k_o12 1.60 / 0.54 / 0.32 ms at j1 = 0 / 1 / 2 against
-        // 1.50 / 0.38 / 0.17 for k_o1 + k_o2 (the k_o1 phases lose their 768-thread, many-workgroup
-        // launch shape); off unless asked for
-        bool o12_on = false;
-        if (const char* e = diag_env("WST_O12")) o12_on = std::atoi(e) != 0;
-#ifndef WST_O12_T
-#define WST_O12_T 512
-#endif
-        std::vector<int> o12t(J, WST_O12_T);
-        threads_override("WST_O12_THREADS", o12t);
-        for (int j1 = plan->rb; j1 + 1 < J && o12_on && max_order >= 2; ++j1) {
-            const int nM1 = g.PM >> j1, nN1 = g.PN >> j1, hld = nN1 / 2 + 1, T = o12t[j1];
-            if (!plan->sq || plan->o2r[j1] || plan->o2_export[j1] || plan->cap[j1] < 24) continue;
-            if ((nM1 / 2) * hld > 8 * T || nM1 * hld > 12 * T) continue;
-            plan->o12[j1] = 1;
-            plan->o12_threads[j1] = T;
-            plan->o12_lds[j1] = std::max(plan->o1_lds[j1], plan->o2_lds[j1]);
-        }
-    }
     for (int j1 = plan->rb; j1 < J; ++j1) {
         plan->o1_threads[j1] = fill_cu(plan->o1_threads[j1], plan->o1_lds[j1]);
         if (plan->o2_lds[j1] > 0) plan->o2_threads[j1] = fill_cu(plan->o2_threads[j1], plan->o2_lds[j1], 768);
@@ -1166,17 +1007,6 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
     const bool do2 = g.max_order >= 2 && j1 < g.J - 1;
     float2* hexp = do2 ? reinterpret_cast<float2*>(base + plan->ws_h_off[j1] * chunk) : nullptr;
     int rc;
-    if (do2 && plan->o12[j1]) {   // k_o1 + k_o2 in one launch (timed in the k_o2 slot)
-        if ((rc = timer.begin(stream)) != WST_OK) return rc;
-        LdsLayout lay1 = plan->o1_lay[j1];
-        lay1.export_full = 1;
-        if (!plan->ops->o12(plan->cap[j1], Launch{dim3(nimg * g.L), dim3(plan->o12_threads[j1]), plan->o12_lds[j1],
-                                                  stream},
-                            plan->dp, lay1, plan->o2_lay[j1], j1, nimg, img0, xhat, d_out, pooled))
-            return fail(WST_ERR_UNSUPPORTED, "k_o12 not compiled for this size class");
-        WST_HIP_CHECK(hipGetLastError());
-        return timer.end(stream, 1 + g.J + j1);
-    }
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
     plan->ops->o1(plan->cap[j1], plan->sq,
                   Launch{dim3(nimg * g.L), dim3(plan->o1_threads[j1]), plan->o1_lds[j1], stream},
@@ -1185,15 +1015,6 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
     if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
     if (!do2) return WST_OK;
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
-    int j2first = j1 + 1;
-    if (plan->o2r[j1]) {   // the j2 = j1 + 1 paths in registers (k_o2r), the rest in k_o2
-        const int n1 = g.PM >> j1;
-        if (!plan->ops->o2r(n1, Launch{dim3(nimg * g.L), dim3(64 * wstdev::kO2rWaves), plan->o2r_lds[j1], stream},
-                            plan->dp, plan->o2r_lay2[j1], plan->o2r_nwl[j1], j1, nimg, img0, hexp, d_out, pooled))
-            return fail(WST_ERR_UNSUPPORTED, "k_o2r not compiled for level size " + std::to_string(n1));
-        WST_HIP_CHECK(hipGetLastError());
-        return timer.end(stream, 1 + g.J + j1);   // k_o2r ran every level of j1
-    }
     if (plan->o2_export[j1]) {   // spectrum exported fully transformed: fold from HBM
         plan->ops->o2(136, 0, 1, Launch{dim3(nimg * g.L * std::max(1, plan->o2x_lay[j1].nsplit)),
                                         dim3(plan->o2x_threads[j1]), plan->o2x_lds[j1], stream},
@@ -1203,7 +1024,7 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
     }
     plan->ops->o2(plan->cap[j1], plan->sq, 0,
                   Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
-                  plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j2first);
+                  plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j1 + 1);
     WST_HIP_CHECK(hipGetLastError());
     return timer.end(stream, 1 + g.J + j1);
 }
@@ -1387,8 +1208,12 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
         ws = sw.ptr;
         wsb = sw.bytes;
     }
-    const int64_t chunk = std::min<int64_t>(static_cast<int64_t>(wsb / plane_ws), plan->max_chunk);
-    if (chunk < 1) return fail(WST_ERR_INVALID, "workspace smaller than one plane's share");
+    const int64_t cap = std::min<int64_t>(static_cast<int64_t>(wsb / plane_ws), plan->max_chunk);
+    if (cap < 1) return fail(WST_ERR_INVALID, "workspace smaller than one plane's share");
+    // balanced chunks: the fewest launches the workspace allows, all of (nearly) equal size (c2's
+    // 3072 planes as 2 x 1536 rather than 2048 + 1024: equal per-plane cost, measured 0.4 % faster)
+    const int64_t nchunks = (nbatch + cap - 1) / cap;
+    const int64_t chunk = (nbatch + nchunks - 1) / nchunks;
     const int inM = plan->dp.pre_pad ? g.PM : g.M, inN = plan->dp.pre_pad ? g.PN : g.N;
     // workspace regions (chunk-sized): Xhat, then each level's half spectra
     unsigned char* base = reinterpret_cast<unsigned char*>(ws);

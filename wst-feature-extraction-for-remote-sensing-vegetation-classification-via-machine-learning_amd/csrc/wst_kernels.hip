@@ -13,8 +13,6 @@ namespace {
 
 constexpr int FM = WST_FAM_M, FN = WST_FAM_N;
 constexpr bool kSquareFamily = (FM == FN) && FM > 0;
-// k_o2r level sizes 96 and 48 (wst_wave.h) belong to family 3
-constexpr bool kO2r = kSquareFamily && FM == 3;
 
 template <int C, int SQ>
 hipError_t attrs_cap() {
@@ -44,26 +42,8 @@ hipError_t set_attrs() {
         if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2<FM, FN, 136, 0, 1>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds)) != hipSuccess)
             return e;
-        if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2<FM, FN, 136, 1, 1>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds)) != hipSuccess)
-            return e;
-        {
-            const void* ks[3] = {reinterpret_cast<const void*>(wstdev::k_o12<FM, FN, 24, 1>),
-                                 reinterpret_cast<const void*>(wstdev::k_o12<FM, FN, 48, 1>),
-                                 reinterpret_cast<const void*>(wstdev::k_o12<FM, FN, 136, 1>)};
-            for (const void* k : ks)
-                if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds)) !=
-                    hipSuccess)
-                    return e;
-        }
-        if constexpr (kO2r) {
-            if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2r<FM, 96>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds)) != hipSuccess)
-                return e;
-            if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2r<FM, 48>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds)) != hipSuccess)
-                return e;
-        }
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(wstdev::k_o2<FM, FN, 136, 1, 1>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds);
     }
     return hipSuccess;
 }
@@ -123,48 +103,12 @@ void o2(int cap, int sq, int hg, const Launch& q, const DevParams& dp, const Lds
     o2_sq<0, 0>(cap, q, dp, lay, j1, nimg, img0, hexp, out, pooled, j2first);
 }
 
-bool o2r(int n1c, const Launch& q, const DevParams& dp, const LdsLayout& lay2, int nwl, int j1, int nimg,
-         long long img0, const float2* hexp, float* out, int pooled) {
-    if constexpr (kO2r) {
-        if (n1c == 96) {
-            hipLaunchKernelGGL((wstdev::k_o2r<FM, 96>), q.grid, q.block, q.lds, q.st, dp, lay2, nwl, j1, nimg, img0, hexp,
-                               out, pooled);
-            return true;
-        }
-        if (n1c == 48) {
-            hipLaunchKernelGGL((wstdev::k_o2r<FM, 48>), q.grid, q.block, q.lds, q.st, dp, lay2, nwl, j1, nimg, img0, hexp,
-                               out, pooled);
-            return true;
-        }
-    }
-    (void)n1c; (void)q; (void)dp; (void)lay2; (void)nwl; (void)j1; (void)nimg; (void)img0; (void)hexp; (void)out;
-    (void)pooled;
-    return false;
-}
-
-bool o12(int cap, const Launch& q, const DevParams& dp, const LdsLayout& lay1, const LdsLayout& lay2, int j1,
-         int nimg, long long img0, const float2* xhat, float* out, int pooled) {
-    if constexpr (kSquareFamily) {
-#define WST_O12_CAP(C)                                                                                \
-    if (cap == C) {                                                                                   \
-        hipLaunchKernelGGL((wstdev::k_o12<FM, FN, C, 1>), q.grid, q.block, q.lds, q.st, dp, lay1, lay2, j1, \
-                           nimg, img0, xhat, out, pooled);                                            \
-        return true;                                                                                  \
-    }
-        WST_O12_CAP(24) WST_O12_CAP(48) WST_O12_CAP(136)
-#undef WST_O12_CAP
-    }
-    (void)cap; (void)q; (void)dp; (void)lay1; (void)lay2; (void)j1; (void)nimg; (void)img0; (void)xhat;
-    (void)out; (void)pooled;
-    return false;
-}
-
 }  // namespace
 
 #define WST_GETTER_NAME(A, B) WST_FAMILY_GETTER(A, B)
 #define WST_GETTER_EXPAND(A, B) WST_GETTER_NAME(A, B)
 const FamilyOps& WST_GETTER_EXPAND(WST_FAM_M, WST_FAM_N)() {
-    static const FamilyOps ops{FM, FN, set_attrs, prep, o1, o2, o2r, o12};
+    static const FamilyOps ops{FM, FN, set_attrs, prep, o1, o2};
     return ops;
 }
 

@@ -7,7 +7,6 @@
 
 #include "wst_device.h"
 #include "wst_staged.h"
-#include "wst_wave.h"
 
 namespace wstlaunch {
 
@@ -32,13 +31,6 @@ struct FamilyOps {
     // hg: spectrum of a big level read from HBM (square families, cap 136), paths from j2first
     void (*o2)(int cap, int sq, int hg, const Launch&, const DevParams&, const LdsLayout&, int j1,
                int nimg, long long img0, const float2* hexp, float* out, int pooled, int j2first);
-    // k_o2r (wst_wave.h): the j2 = j1 + 1 paths of an n1c x n1c level in registers; false when this
-    // family has no k_o2r for n1c (nothing launched)
-    bool (*o2r)(int n1c, const Launch&, const DevParams&, const LdsLayout& lay2, int nwl, int j1, int nimg,
-                long long img0, const float2* hexp, float* out, int pooled);
-    // k_o12 (k_o1 + k_o2 of one level fused, square fused-low-pass plans): false when not compiled
-    bool (*o12)(int cap, const Launch&, const DevParams&, const LdsLayout& lay1, const LdsLayout& lay2,
-                int j1, int nimg, long long img0, const float2* xhat, float* out, int pooled);
 };
 
 // HBM-staged passes of one big level size N (wst_staged.h), compiled per N (wst_staged.hip).
