@@ -469,6 +469,14 @@ constexpr int kLpOM = 8;  // row stride of the GM tap matrices = largest oM of t
 // 16x16x4 form: A[m = lane & 15][k = lane >> 4], B[k = lane >> 4][n = lane & 15],
 // D[row = 4 (lane >> 4) + i][col = lane & 15].  Ends with a barrier.
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+// The .x / .y half of an LDS float2 read as one ds_read_b64: the bank argument of the MFMA
+// low-pass's operand reads holds for 8-byte reads (the compiler would narrow a plain .x to
+// ds_read_b32, which maps a 32-lane half onto 16 even banks: 2-way conflicts at best).
+__device__ __forceinline__ float lds_half64(const float2* q, int hi) {
+    unsigned long long w = *reinterpret_cast<const unsigned long long*>(q);
+    asm volatile("" : "+v"(w));
+    return __uint_as_float(static_cast<unsigned>(hi ? (w >> 32) : w));
+}
 // S addressing: map b, value i = a * oN + c at S[b * s_bs + i * s_es] (default: contiguous maps;
 // k_o2 passes the .x slots of the arrays U themselves, free once step 1 has read them).
 __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int rows, int cols, int ld,
@@ -476,10 +484,12 @@ __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int 
                                                  const float* __restrict__ GN, int oMp, int oNp,
                                                  int oM, int oN, float* S, int s_bs = -1, int s_es = 1) {
     if (s_bs < 0) s_bs = oM * oN;
-    constexpr int KU = 4;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const int li = lane & 15, lk = lane >> 4;
     const int nmt = (rows + 15) >> 4, nnt = oNp >> 4, nat = oMp >> 4;
+    // K parts (host: wst_hip.hip lpw): 64-row blocks (step u reads row 64 b + u + 16 lk: the
+    // U operand reads are conflict-free ds_read_b64), 16-row blocks (row 16 b + 4 u + lk), single
+    // 4-row steps; no MFMA is issued on an all-padding step (68 rows = 64 + 4 x 1: 17 steps)
     // 1. T = U GN
     const int ntask1 = nb * nmt * nnt;
     for (int t = wave; t < ntask1; t += nw) {
@@ -490,19 +500,36 @@ __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int 
         const int p = mt * 16 + li;
         const bool pok = p < rows;
         const float2* urow = Ub + (pok ? p : rows - 1) * ld;
-        const int nfb = cols >> 4;
-        const float4* gblk = reinterpret_cast<const float4*>(GN) + nt * 64 + lane;
-        const float* gcol = GN + nfb * nnt * 256 - 16 * nfb * oNp + nt * 16 + li;   // tail rows
+        const int n64 = cols >> 6, n16 = (cols - 64 * n64) >> 4;
+        const float4* g64 = reinterpret_cast<const float4*>(GN) + (nt * 64 + lane) * 4;
+        const float4* g16 = reinterpret_cast<const float4*>(GN) + n64 * nnt * 256 + nt * 64 + lane;
+        const float* gcol = GN + (n64 * 4 + n16) * nnt * 256 - (64 * n64 + 16 * n16) * oNp + nt * 16 + li;
         f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-        // whole 16-row K blocks (one 16-byte tap load per lane feeds 4 MFMAs), then the remaining
-        // K steps one by one: no MFMA is issued on an all-padding step (68 = 17 x 4: 17 steps, not
-        // the 20 of five 16-wide blocks)
         int q0 = 0;
-        for (int blk = 0; blk < nfb; ++blk, q0 += 4 * KU) {
-            const float4 b4 = gblk[blk * nnt * 64];
-            float a[KU];
+        for (int blk = 0; blk < n64; ++blk, q0 += 64) {
 #pragma unroll
-            for (int u = 0; u < KU; ++u) a[u] = pok ? urow[q0 + 4 * u + lk].x : 0.f;
+            for (int h = 0; h < 2; ++h) {   // two halves of 8 steps (registers)
+                const float4 b4a = g64[blk * nnt * 256 + 2 * h];
+                const float4 b4b = g64[blk * nnt * 256 + 2 * h + 1];
+                const float bv[8] = {b4a.x, b4a.y, b4a.z, b4a.w, b4b.x, b4b.y, b4b.z, b4b.w};
+                float a[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const float v = lds_half64(urow + q0 + 8 * h + u + 16 * lk, 0);
+                    a[u] = pok ? v : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u += 2) {
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], bv[u], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u + 1], bv[u + 1], acc1, 0, 0, 0);
+                }
+            }
+        }
+        for (int blk = 0; blk < n16; ++blk, q0 += 16) {
+            const float4 b4 = g16[blk * nnt * 64];
+            float a[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) a[u] = pok ? urow[q0 + 4 * u + lk].x : 0.f;
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b4.x, acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b4.y, acc1, 0, 0, 0);
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b4.z, acc0, 0, 0, 0);
@@ -533,16 +560,36 @@ __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int 
         const float2* Ub = U + b * bs;
         const int c = ct * 16 + li;
         const bool cok = c < oN;
-        const int nfb = rows >> 4;
-        const float4* gblk = reinterpret_cast<const float4*>(GM) + at * 64 + lane;
-        const float* gcol = GM + nfb * nat * 256 - 16 * nfb * oMp + at * 16 + li;   // tail rows
+        const int n64 = rows >> 6, n16 = (rows - 64 * n64) >> 4;
+        const float4* g64 = reinterpret_cast<const float4*>(GM) + (at * 64 + lane) * 4;
+        const float4* g16 = reinterpret_cast<const float4*>(GM) + n64 * nat * 256 + at * 64 + lane;
+        const float* gcol = GM + (n64 * 4 + n16) * nat * 256 - (64 * n64 + 16 * n16) * oMp + at * 16 + li;
         f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
         int p0 = 0;
-        for (int blk = 0; blk < nfb; ++blk, p0 += 4 * KU) {
-            const float4 a4 = gblk[blk * nat * 64];
-            float bv[KU];
+        for (int blk = 0; blk < n64; ++blk, p0 += 64) {
 #pragma unroll
-            for (int u = 0; u < KU; ++u) bv[u] = cok ? Ub[(p0 + 4 * u + lk) * ld + c].y : 0.f;
+            for (int h = 0; h < 2; ++h) {
+                const float4 a4a = g64[blk * nat * 256 + 2 * h];
+                const float4 a4b = g64[blk * nat * 256 + 2 * h + 1];
+                const float av[8] = {a4a.x, a4a.y, a4a.z, a4a.w, a4b.x, a4b.y, a4b.z, a4b.w};
+                float bv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const float v = lds_half64(Ub + (p0 + 8 * h + u + 16 * lk) * ld + (cok ? c : 0), 1);
+                    bv[u] = cok ? v : 0.f;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u += 2) {
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u + 1], bv[u + 1], acc1, 0, 0, 0);
+                }
+            }
+        }
+        for (int blk = 0; blk < n16; ++blk, p0 += 16) {
+            const float4 a4 = g16[blk * nat * 64];
+            float bv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) bv[u] = cok ? Ub[(p0 + 4 * u + lk) * ld + c].y : 0.f;
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.x, bv[0], acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.y, bv[1], acc1, 0, 0, 0);
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a4.z, bv[2], acc0, 0, 0, 0);

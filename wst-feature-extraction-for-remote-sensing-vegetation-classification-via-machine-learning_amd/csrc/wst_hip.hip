@@ -573,9 +573,14 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     // wide tap matrices for the MFMA low-pass (lds_lowpass_mfma), columns padded to x16:
     //   [2r + d] level r in physical order (r < J), [2J + d] level 0 in natural order (k_prep)
     const int oMp = (g.oM + 15) & ~15, oNp = (g.oN + 15) & ~15;
-    // Stored in the MFMA operand order: each 16-row K block of a 16-column tile is 64 lanes x 4
-    // K steps (lane = 16 (q & 3) + column, the 4 values of a lane contiguous: one 16-byte load
-    // feeds 4 MFMAs); rows past the last whole block follow row-major.
+    // Stored in the MFMA operand order, K (the rows q) in three parts:
+    //  * 64-row blocks: per 16-column tile 64 lanes x 16 K steps, step u of lane (lk = lane >> 4)
+    //    taking row 64 b + u + 16 lk (the lanes of one 32-lane half read U rows 16 apart: for any
+    //    odd row stride ld those 32 rows fall on distinct bank pairs, so the kernel's ds_read_b64
+    //    operand reads are conflict-free; with rows 4 u + lk they were 2-way);
+    //  * then 16-row blocks: 64 lanes x 4 K steps, row 16 b + 4 u + lk;
+    //  * the rows past the last whole block row-major.
+    // A lane's values of a block are contiguous (16-byte loads, each feeding 4 MFMAs).
     std::vector<float> lpw;
     std::vector<int> lpw_off(2 * static_cast<size_t>(J + 1), 0);
     for (int slot = 0; slot <= J; ++slot)
@@ -592,13 +597,18 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
             };
             while (lpw.size() % 4) lpw.push_back(0.f);
             lpw_off[2 * slot + d] = static_cast<int>(lpw.size());
-            const int nfb = n / 16, ntile = np_ / 16;
-            for (int b = 0; b < nfb; ++b)
+            const int n64 = n / 64, n16 = (n - 64 * n64) / 16, ntile = np_ / 16;
+            for (int b = 0; b < n64; ++b)
+                for (int tl = 0; tl < ntile; ++tl)
+                    for (int lane = 0; lane < 64; ++lane)
+                        for (int u = 0; u < 16; ++u)
+                            lpw.push_back(tap(64 * b + u + 16 * (lane >> 4), 16 * tl + (lane & 15)));
+            for (int b = 0; b < n16; ++b)
                 for (int tl = 0; tl < ntile; ++tl)
                     for (int lane = 0; lane < 64; ++lane)
                         for (int u = 0; u < 4; ++u)
-                            lpw.push_back(tap(16 * b + 4 * u + (lane >> 4), 16 * tl + (lane & 15)));
-            for (int q = 16 * nfb; q < n; ++q)
+                            lpw.push_back(tap(64 * n64 + 16 * b + 4 * u + (lane >> 4), 16 * tl + (lane & 15)));
+            for (int q = 64 * n64 + 16 * n16; q < n; ++q)
                 for (int a = 0; a < np_; ++a) lpw.push_back(tap(q, a));
         }
     // twiddles exp(-2 pi i k / n) per level and side; pool order: M levels 0..J, then N levels
