@@ -437,20 +437,26 @@ __global__ void k_u8_to_chw(const uint8_t* __restrict__ in, long long nimg, int 
 }
 
 // ---- measurement probes (bench.py: BW_meas, FP32_meas of SURVEY.md §8(d)) ----
-// Streaming copy, 16 B per lane per access, four accesses in flight per lane, grid-stride.
+// Streaming copy: every workgroup copies one contiguous 8 KiB tile, 16 B per lane, two
+// non-temporal loads in flight per lane before their stores.  Measured on MI355X (2 GiB -> 2 GiB,
+// read + written bytes; tools/micro/copy_probe.hip): grid-stride forms 4.4-4.7 TB/s, contiguous
+// 64 / 32 / 16 / 8 KiB tiles with nt loads 5.66 / 5.84 / 5.74 / 6.00 TB/s; hipMemcpy D2D 4.8 TB/s.
 typedef float v4f __attribute__((ext_vector_type(4)));
+constexpr long long kProbeTile = 512;    // float4 per workgroup tile (8 KiB)
 __global__ void __launch_bounds__(256) k_probe_copy(const v4f* __restrict__ src, v4f* __restrict__ dst,
                                                     long long n) {
-    const long long stride = static_cast<long long>(gridDim.x) * blockDim.x;
-    long long i = blockIdx.x * static_cast<long long>(blockDim.x) + threadIdx.x;
-    for (; i + 3 * stride < n; i += 4 * stride) {
-        const v4f a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
+    constexpr int U = 4;
+    const long long b0 = blockIdx.x * kProbeTile;
+    const long long e = b0 + kProbeTile < n ? b0 + kProbeTile : n;
+    for (long long i = b0 + threadIdx.x; i < e; i += U * 256) {
+        v4f t[U];
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            if (i + k * 256 < e) t[k] = __builtin_nontemporal_load(src + i + k * 256);
+#pragma unroll
+        for (int k = 0; k < U; ++k)
+            if (i + k * 256 < e) __builtin_nontemporal_store(t[k], dst + i + k * 256);
     }
-    for (; i < n; i += stride) dst[i] = src[i];
 }
 // 32 independent FMA chains per lane, the step loop unrolled by 4 (loop overhead < 2 % of the
 // VALU issue); a, b are runtime values so nothing folds.
@@ -594,7 +600,8 @@ int wst_probe_copy(const void* d_src, void* d_dst, size_t bytes, void* stream) {
         (reinterpret_cast<uintptr_t>(d_dst) & 15))
         return aux_fail(WST_ERR_INVALID, "copy probe needs 16-byte aligned buffers and size");
     const long long n = static_cast<long long>(bytes / 16);
-    hipLaunchKernelGGL(k_probe_copy, dim3(256 * 16), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+    hipLaunchKernelGGL(k_probe_copy, dim3(static_cast<unsigned>((n + kProbeTile - 1) / kProbeTile)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream),
                        static_cast<const v4f*>(d_src), static_cast<v4f*>(d_dst), n);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return aux_fail(WST_ERR_HIP, hipGetErrorString(e));
