@@ -96,6 +96,11 @@ int wst_workspace_bytes(const wst_plan* plan, int64_t nbatch, size_t* bytes);
  * geometries with HBM-staged levels, whose workspace is tens of MB per plane).  wst_forward
  * never processes more planes than this per chunk; size the workspace for
  * min(nbatch, preferred) planes.  (No kymatio counterpart: sizing helper of the batched ABI.) */
+/* Internal workspaces (wst_forward with d_workspace == NULL) the plan holds: one per stream,
+ * at most 4 streams (a new stream evicts the least recently used buffer once its last work has
+ * completed).  Lets callers and tests bound the plan's device memory. */
+int wst_internal_workspaces(const wst_plan* plan, int* count, size_t* bytes);
+
 int wst_preferred_batch(const wst_plan* plan, int64_t* planes);
 
 /*

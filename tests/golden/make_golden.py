@@ -29,6 +29,10 @@ CASES = {
     "f3_rgb128_J2_L8": (1, 128, 128, 2, 8, 2, "reference real geometry 128x128 J=2 (P=136), 1 channel"),
     "c5_ms256_J6_L12": (1, 256, 256, 6, 12, 2, "BASELINE config 5 geometry, 1 band"),
     "staged192_gray128_J5_L8": (1, 128, 128, 5, 8, 2, "P=192: one HBM-staged level (192^2) then LDS levels"),
+    "staged384_gray256_J6_L7": (1, 256, 256, 6, 7, 2, "two HBM-staged levels (384^2, 192^2), odd L: the "
+                                "all-paths s = 2 row pass with an unpaired last path"),
+    "rectstaged_256x128_J4_L8": (1, 256, 128, 4, 8, 2, "rectangular plane needing a staged level (288 x 160)"),
+    "staged224_gray192_J4_L8": (1, 192, 192, 4, 8, 2, "P=224 (family 7): staged level size 224"),
 }
 
 

@@ -232,3 +232,32 @@ def test_family_geometries_against_oracle(M, J, L):
     got = NpS(J=J, shape=(M, M), L=L)(x)
     ref = kr.Scattering2D(J=J, shape=(M, M), L=L)(x)
     assert_parity(got, ref, what=f"{M}x{M} J={J} L={L}")
+
+
+def test_internal_workspace_streams_bounded_and_bitwise_equal():
+    # per-stream internal workspaces are capped (LRU, evicted once their work is done);
+    # every stream's result equals the caller-workspace result bit for bit
+    d, x = golden_input("c2_rgb64_J4_L8")
+    plan = _lib.Plan(64, 64, 4, 8)
+    xt = torch.from_numpy(np.concatenate([x] * 4, 0)).cuda()
+    B = xt.shape[0]
+    ref = torch.empty((B, plan.K, plan.Mo, plan.No), device="cuda")
+    ws = torch.empty(plan.workspace_bytes(B), dtype=torch.uint8, device="cuda")
+    plan.forward(xt.data_ptr(), B, ref.data_ptr(), False, ws.data_ptr(), ws.numel(),
+                 torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(6)]
+    outs = []
+    for rep in range(2):
+        for s in streams:
+            o = torch.empty_like(ref)
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                plan.forward(xt.data_ptr(), B, o.data_ptr(), False, 0, 0, s.cuda_stream)
+            outs.append((s, o))
+            n, nbytes = plan.internal_workspaces()
+            assert 1 <= n <= 4, n
+            assert nbytes <= 4 * plan.workspace_bytes(B)
+    torch.cuda.synchronize()
+    for _, o in outs:
+        assert torch.equal(o, ref)

@@ -108,7 +108,44 @@ def test_c5_full_size_properties():
     assert err <= 2 * TOL, err
 
 
-def test_large_rectangular_plane_is_unsupported():
+@pytest.mark.parametrize("name,M,N,J,L", [("rectstaged_256x128_J4_L8", 256, 128, 4, 8),
+                                           ("staged224_gray192_J4_L8", 192, 192, 4, 8),
+                                           ("staged384_gray256_J6_L7", 256, 256, 6, 7)])
+def test_staged_general_geometries_chunking_and_parity(name, M, N, J, L):
+    """Staged planes outside the square compiled-family route: rectangular (288 x 160 padded, row
+    and column passes of different lengths, 144 x 80 level 1 with a runtime-length row pass),
+    a padded size without a compiled staged FFT (224^2: generic DFT passes, 12 x 12 output maps)
+    and odd L (unpaired last path in the all-paths s = 2 fold).  Golden parity at several batch
+    positions, chunking invariance."""
+    d, x = golden(name)
+    ref = d["S"][0]
+    rng = np.random.default_rng(5)
+    xs = rng.integers(0, 256, (4, M, N), dtype=np.uint8).astype(np.float32) / 255
+    pos = [0, 3]
+    for i in pos:
+        xs[i] = x[0]
+    plan = _lib.Plan(M, N, J, L)
+    xt = torch.from_numpy(xs).cuda()
+    full = forward(plan, xt)
+    small = forward(plan, xt, ws_planes=3)        # 2 chunks: 3 + 1 planes
+    assert torch.equal(full, small), "chunked staged run differs"
+    for i in pos:
+        assert_parity(full[i].cpu().numpy()[None], ref[None], TOL, f"{name} @ {i}")
+    assert torch.isfinite(full).all()
+
+
+def test_staged_tall_plane_against_oracle():
+    """The transposed orientation of the rectangular case (160 x 288 padded: row passes of 288
+    points, column passes of 160), order 2, checked against the oracle directly."""
+    x = np.random.default_rng(6).integers(0, 256, (1, 128, 256), dtype=np.uint8).astype(np.float32) / 255
+    ref = kr.Scattering2D(J=4, shape=(128, 256), L=4)(x)
+    got = NpS(J=4, shape=(128, 256), L=4)(x)
+    assert got.shape == ref.shape == (1, 1 + 4 * 4 + 16 * 6, 8, 16)
+    assert_parity(got, ref, TOL, "staged 128x256")
+
+
+def test_staged_wide_output_maps_are_unsupported():
     with pytest.raises(_lib.WSTError) as e:
-        _lib.Plan(256, 128, 4, 8)                  # 288 x 160 padded: staged needs square
+        _lib.Plan(512, 512, 4, 8)                  # 544^2 padded, 32 x 32 output maps
     assert e.value.code == _lib.WST_ERR_UNSUPPORTED
+    assert "16 wide" in str(e.value)

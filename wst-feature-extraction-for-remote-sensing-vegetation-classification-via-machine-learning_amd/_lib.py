@@ -23,6 +23,7 @@ EXPORTS = (
     "wst_abi_version", "wst_last_error", "wst_default_convention", "wst_plan_create",
     "wst_plan_create_ex", "wst_plan_destroy",
     "wst_output_shape", "wst_padded_shape", "wst_workspace_bytes", "wst_preferred_batch",
+    "wst_internal_workspaces",
     "wst_forward",
     "wst_forward_profiled", "wst_host_filter", "wst_host_filter_ex", "wst_host_fft_lines",
     "wst_salt_pepper_counts", "wst_noise_apply", "wst_noise_generate", "wst_advanced_stats",
@@ -126,6 +127,8 @@ def load() -> ctypes.CDLL:
         lib.wst_aux_last_error.argtypes = []
         lib.wst_preferred_batch.restype = c_int
         lib.wst_preferred_batch.argtypes = [c_vp, ctypes.POINTER(c_i64)]
+        lib.wst_internal_workspaces.restype = c_int
+        lib.wst_internal_workspaces.argtypes = [c_vp, ctypes.POINTER(c_int), ctypes.POINTER(c_sz)]
         lib.wst_forward.restype = c_int
         lib.wst_forward.argtypes = [c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_sz, c_vp]
         lib.wst_forward_profiled.restype = c_int
@@ -218,6 +221,12 @@ class Plan:
         b = ctypes.c_int64()
         check(load().wst_preferred_batch(self._h, ctypes.byref(b)))
         return b.value
+
+    def internal_workspaces(self):
+        """(count, bytes) of the per-stream internal workspaces (wst_internal_workspaces)."""
+        n, b = ctypes.c_int(), ctypes.c_size_t()
+        check(load().wst_internal_workspaces(self._h, ctypes.byref(n), ctypes.byref(b)))
+        return n.value, b.value
 
     def forward(self, d_in: int, nbatch: int, d_out: int, pooled: bool, d_ws: int, ws_bytes: int,
                 stream: int) -> None:

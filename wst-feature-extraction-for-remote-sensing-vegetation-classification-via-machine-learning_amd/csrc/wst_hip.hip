@@ -60,12 +60,14 @@ int family_of(int P) {
                            o == 15 || o == 17 || o == 27);
     return compiled ? o : 0;
 }
+// staged passes over lines of n points: the compiled FFT of that length, else the runtime-length
+// instantiation (generic DFT)
 const wstlaunch::BigOps* big_ops(int n) {
 #define WST_BIG_OPS(N) \
     if (n == N) return &wstlaunch::WST_BIG_GETTER(N)();
     WST_BIG_SIZES(WST_BIG_OPS)
 #undef WST_BIG_OPS
-    return nullptr;
+    return &wstlaunch::WST_BIG_GETTER(0)();
 }
 const FamilyOps* family_ops(int fm, int fn) {
 #define WST_PAIR_OPS(A, B) \
@@ -77,13 +79,14 @@ const FamilyOps* family_ops(int fm, int fn) {
 int cap_for(int n) { return n <= 12 ? 12 : n <= 24 ? 24 : n <= 48 ? 48 : 136; }
 constexpr int kBigRows = 8;   // rows per row-pass workgroup of the staged levels (kRowFold2: 2 paths)
 // Rows per row-pass workgroup by mode: the LDS holds 2 kBigRows lines, so the single-path modes
-// take 2 kBigRows rows and kRowReal2 (two rows per complex line) 4 kBigRows, when n allows: at
-// n = 384 the 8-line FFT stages left half the 256 threads idle (kRowReal2: three quarters).
-int big_rows(int mode, int n) {
-    const int want = mode == wstbig::kRowFold2 ? kBigRows : mode == wstbig::kRowReal2 ? 4 * kBigRows : 2 * kBigRows;
-    for (int r = want; r > kBigRows; r /= 2)
-        if (n % r == 0) return r;
-    return kBigRows;
+// take 2 kBigRows rows and kRowReal2 (two rows per complex line) 4 kBigRows, when the row count
+// allows (at n = 384 the 8-line FFT stages left half the 256 threads idle, kRowReal2 three
+// quarters); otherwise the largest power of two dividing it (the grid has nrows / rows blocks;
+// order-2 levels have even row counts, so kRowReal2 keeps at least one row pair).
+int big_rows(int mode, int nrows) {
+    int r = mode == wstbig::kRowFold2 ? kBigRows : mode == wstbig::kRowReal2 ? 4 * kBigRows : 2 * kBigRows;
+    while (r > 1 && nrows % r != 0) r /= 2;
+    return r;
 }
 
 size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
@@ -167,8 +170,12 @@ struct wst_plan {
     std::vector<LdsLayout> o1_lay, o2_lay;
     // HBM-staged leading levels (n > kBigMinN): wst_staged.h
     int rb = 0;
-    int oms = 4;                                  // tap-matrix row stride
-    std::vector<const wstlaunch::BigOps*> big;    // per staged level
+    int nst = 0;                                  // levels with staged passes: rb, or J when the
+                                                  // staged j1's order-2 levels all run staged
+    int oms = 4;                                  // tap-matrix row stride (LDS-resident kernels)
+    int noms = 4;                                 // row stride of the natural tap matrices (staged)
+    std::vector<const wstlaunch::BigOps*> big_r;  // per staged level: row lines (PN >> r points)
+    std::vector<const wstlaunch::BigOps*> big_c;  //   column lines (PM >> r points)
     std::vector<int> lpn_off;                     // natural tap matrices: [2r] GM_r, [2r+1] GN_r
     float* d_lpn = nullptr;
     float* d_lpw = nullptr;                       // wide tap matrices (MFMA low-pass)
@@ -197,7 +204,10 @@ struct wst_plan {
     struct StreamWs {
         void* ptr = nullptr;
         size_t bytes = 0;
+        hipEvent_t done = nullptr;     // recorded after the last call's work on this buffer
+        unsigned long long tick = 0;   // last use (LRU eviction)
     };
+    mutable unsigned long long ws_tick = 0;
     mutable std::mutex ws_mu;
     mutable std::map<hipStream_t, StreamWs> ws_by_stream;
 };
@@ -225,8 +235,11 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_lpn);
     (void)hipFree(p->d_lpw);
     (void)hipFree(p->d_lpw_off);
-    for (auto& kv : p->ws_by_stream)
+    for (auto& kv : p->ws_by_stream) {
+        if (kv.second.done) (void)hipEventSynchronize(kv.second.done);
         if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+        if (kv.second.done) (void)hipEventDestroy(kv.second.done);
+    }
     delete p;
 }
 
@@ -301,6 +314,8 @@ size_t layout(LdsLayout& lay, size_t data_a, size_t data_b, const TableOffsets& 
     o += 16 * sizeof(float);
     return o;
 }
+
+constexpr size_t kMaxStreamWs = 4;   // streams that keep an internal workspace per plan
 
 // paths per order-2 batch at level j2 (mirrors k_o2)
 constexpr int kHgSplit = 3;   // k_o2 HG workgroups per (plane, theta1)
@@ -555,7 +570,9 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
             t.lpt_len[2 * r + d] = n * oms;
         }
     t.lpt_off.back() = static_cast<int>(lpt.size());
-    // the same tap matrices in natural order (HBM-staged levels use natural-order transforms)
+    // the same tap matrices in natural order (HBM-staged levels use natural-order transforms); row
+    // stride noms >= max(oM, oN) (the staged passes hold output maps up to kBigMaxO wide)
+    const int noms = std::max(oms, (std::max(g.oM, g.oN) + 3) & ~3);
     std::vector<float> lpn;
     plan->lpn_off.assign(2 * static_cast<size_t>(J), 0);
     for (int r = 0; r < J; ++r)
@@ -566,10 +583,11 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
             const auto& h = d == 0 ? fb.hM[r] : fb.hN[r];
             plan->lpn_off[2 * r + d] = static_cast<int>(lpn.size());
             for (int p = 0; p < n; ++p)
-                for (int a = 0; a < oms; ++a)
+                for (int a = 0; a < noms; ++a)
                     lpn.push_back(a < no ? static_cast<float>(h[((sdec * (a + 1) - p) % n + n) % n]) : 0.f);
         }
     plan->oms = oms;
+    plan->noms = noms;
     // wide tap matrices for the MFMA low-pass (lds_lowpass_mfma), columns padded to x16:
     //   [2r + d] level r in physical order (r < J), [2J + d] level 0 in natural order (k_prep)
     const int oMp = (g.oM + 15) & ~15, oNp = (g.oN + 15) & ~15;
@@ -701,38 +719,46 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     // leading levels too large for the LDS-resident kernels run HBM-staged (wst_staged.h)
     while (plan->rb < J && std::max(g.PM, g.PN) >> plan->rb > wstbig::kBigMinN) ++plan->rb;
     if (plan->rb > 0) {
-        if (g.PM != g.PN || !plan->sq)
+        if (std::max(g.oM, g.oN) > wstbig::kBigMaxO)
             return fail(WST_ERR_UNSUPPORTED,
                         "padded plane " + std::to_string(g.PM) + "x" + std::to_string(g.PN) +
-                            " needs HBM-staged levels, implemented for square planes of a compiled "
-                            "FFT family with M / 2^J <= 8 only");
-        plan->big.assign(plan->rb, nullptr);
-        for (int r = 0; r < plan->rb; ++r)
-            if (!(plan->big[r] = big_ops(g.PM >> r)))
-                return fail(WST_ERR_UNSUPPORTED, "no HBM-staged FFT compiled for level size " +
-                                                     std::to_string(g.PM >> r));
-        plan->big_rows_lds.assign(plan->rb, 0);
-        plan->big_cols_lds.assign(plan->rb, 0);
+                            " needs HBM-staged levels, whose low-pass passes hold output maps up to " +
+                            std::to_string(wstbig::kBigMaxO) + " wide (here " + std::to_string(g.oM) +
+                            "x" + std::to_string(g.oN) + ")");
+        // square compiled-family planes (sq) fold the order-2 levels from rb on out of the global
+        // spectrum (k_o2 HG); any other plane runs every order-2 level of a staged j1 staged
+        plan->nst = plan->sq ? plan->rb : J;
+        const int nst = plan->nst;
+        plan->big_r.assign(nst, nullptr);
+        plan->big_c.assign(nst, nullptr);
+        plan->big_rows_lds.assign(nst, 0);
+        plan->big_cols_lds.assign(nst, 0);
+        for (int r = 0; r < nst; ++r) {
+            const size_t nm = static_cast<size_t>(g.PM >> r), nn = static_cast<size_t>(g.PN >> r);
+            plan->big_r[r] = big_ops(g.PN >> r);
+            plan->big_c[r] = big_ops(g.PM >> r);
+            plan->big_rows_lds[r] = (nn + 2 * kBigRows * (nn | 1)) * sizeof(float2);
+            plan->big_cols_lds[r] = (nm + wstbig::kColTile * (nm | 1)) * sizeof(float2) +
+                                    nm * static_cast<size_t>(noms) * sizeof(float);   // + tap matrix
+            if (std::max(plan->big_rows_lds[r], plan->big_cols_lds[r]) > static_cast<size_t>(kMaxLds))
+                return fail(WST_ERR_UNSUPPORTED, "level " + std::to_string(r) + " (" + std::to_string(nm) + "x" +
+                                                     std::to_string(nn) + ") exceeds the staged passes' " +
+                                                     "LDS line tiles (160 KiB per CU)");
+        }
         // the all-paths s = 2 order-2 row pass: rows x L paths of lines, four workgroups per CU (c5:
         // 2 rows, 28.96 -> 27.92 ms against 4 rows at two workgroups per CU; 1 row: 28.39)
-        plan->fold_all_rows.assign(plan->rb, 0);
-        plan->fold_all_lds.assign(plan->rb, 0);
-        for (int r = 1; r < plan->rb; ++r) {
-            const size_t n = static_cast<size_t>(g.PM >> r);
+        plan->fold_all_rows.assign(nst, 0);
+        plan->fold_all_lds.assign(nst, 0);
+        for (int r = 1; r < nst; ++r) {
+            const size_t nm = static_cast<size_t>(g.PM >> r), nn = static_cast<size_t>(g.PN >> r);
             for (int rows = 4; rows >= 1; rows /= 2) {
-                const size_t lds = (n + static_cast<size_t>(L) * rows * (n | 1)) * sizeof(float2);
-                if (n % rows == 0 && lds <= static_cast<size_t>(kMaxLds) / 4) {
+                const size_t lds = (nn + static_cast<size_t>(L) * rows * (nn | 1)) * sizeof(float2);
+                if (nm % rows == 0 && lds <= static_cast<size_t>(kMaxLds) / 4) {
                     plan->fold_all_rows[r] = rows;
                     plan->fold_all_lds[r] = lds;
                     break;
                 }
             }
-        }
-        for (int r = 0; r < plan->rb; ++r) {
-            const size_t n = static_cast<size_t>(g.PM >> r);
-            plan->big_rows_lds[r] = (n + 2 * kBigRows * (n | 1)) * sizeof(float2);
-            plan->big_cols_lds[r] = (n + wstbig::kColTile * (n | 1)) * sizeof(float2) +
-                                    n * static_cast<size_t>(oms) * sizeof(float);   // + tap matrix
         }
     } else {
         plan->prep_lds = layout(plan->prep_lay, static_cast<size_t>(g.PM) * odd_ld(g.PN) * sizeof(float2),
@@ -760,21 +786,21 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     plan->hg_j2first.assign(J, J);
     size_t tmp_c = 0, part_n = static_cast<size_t>(g.PM);
     for (int j1 = 0; j1 < plan->rb; ++j1) {
-        // staged order 1 (+ U1hat for order 2); order-2 paths staged while j2 < rb, then k_o2 HG
-        const size_t n1 = static_cast<size_t>(g.PM >> j1);
+        // staged order 1 (+ U1hat for order 2); order-2 paths staged while j2 < nst, then k_o2 HG
+        const size_t m1 = static_cast<size_t>(g.PM >> j1), n1 = static_cast<size_t>(g.PN >> j1);
         const bool do2 = max_order >= 2 && j1 < J - 1;
-        tmp_c = std::max(tmp_c, static_cast<size_t>(L) * n1 * n1);
+        tmp_c = std::max(tmp_c, static_cast<size_t>(L) * m1 * n1);
         part_n = std::max(part_n, static_cast<size_t>(L) * n1);
         if (!do2) continue;
         plan->ws_hbig[j1] = wsp;
-        wsp += align16(static_cast<size_t>(L) * n1 * (n1 / 2 + 1) * sizeof(float2));
-        plan->ws_ureal = std::max(plan->ws_ureal, static_cast<size_t>(L) * n1 * n1 * sizeof(float));
-        for (int j2 = j1 + 1; j2 < plan->rb; ++j2) {
-            const size_t n2 = static_cast<size_t>(g.PM >> j2);
-            tmp_c = std::max(tmp_c, static_cast<size_t>(L) * n2 * n2);
+        wsp += align16(static_cast<size_t>(L) * m1 * (n1 / 2 + 1) * sizeof(float2));
+        plan->ws_ureal = std::max(plan->ws_ureal, static_cast<size_t>(L) * m1 * n1 * sizeof(float));
+        for (int j2 = j1 + 1; j2 < plan->nst; ++j2) {
+            const size_t m2 = static_cast<size_t>(g.PM >> j2), n2 = static_cast<size_t>(g.PN >> j2);
+            tmp_c = std::max(tmp_c, static_cast<size_t>(L) * m2 * n2);
             part_n = std::max(part_n, static_cast<size_t>(L) * L * n2);   // every theta1's partials
         }
-        const int j2f = std::max(j1 + 1, plan->rb);
+        const int j2f = std::max(j1 + 1, plan->nst);
         plan->hg_j2first[j1] = j2f;
         if (j2f >= J) continue;
         // two paths of the first resident level (the smaller levels batch as many as fit)
@@ -811,7 +837,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         plan->ws_ureal = wsp;
         wsp += align16(ureal_bytes);
         plan->ws_part = wsp;
-        wsp += align16(part_n * oms * sizeof(float));
+        wsp += align16(part_n * noms * sizeof(float));
         plan->ws_csum = wsp;
         wsp += align16(part_n * sizeof(float));
         plan->ws_mean = wsp;
@@ -882,9 +908,9 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     if (const char* e = diag_env("WST_O2_EXPORT")) export_on = std::atoi(e) != 0;
     if (const char* e = diag_env("WST_FOLD_ALL")) {   // 0: per-pair passes; r > 0: r rows per workgroup
         const int r = std::atoi(e);
-        for (int k = 0; k < plan->rb; ++k) {
+        for (int k = 0; k < plan->nst; ++k) {
             if (plan->fold_all_rows[k] == 0) continue;
-            const size_t n = static_cast<size_t>(g.PM >> k);
+            const size_t n = static_cast<size_t>(g.PN >> k);
             plan->fold_all_rows[k] = r;
             plan->fold_all_lds[k] = (n + static_cast<size_t>(L) * std::max(r, 1) * (n | 1)) * sizeof(float2);
         }
@@ -927,10 +953,21 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     threads_override("WST_O2_THREADS", plan->o2_threads);
     threads_override("WST_O2X_THREADS", plan->o2x_threads);
     threads_override("WST_HG_THREADS", plan->hg_threads);
+    // k_o1's in-place Hermitian split of an exported spectrum holds 8 items per thread: a thread
+    // count lowered by an override would silently drop items, so the plan fails instead
+    for (int j1 = plan->rb; j1 + 1 < J; ++j1)
+        if (plan->o1_lay[j1].export_full &&
+            static_cast<size_t>((g.PM >> j1) / 2) * ((g.PN >> j1) / 2 + 1) > 8 * static_cast<size_t>(plan->o1_threads[j1]))
+            return fail(WST_ERR_INVALID, "k_o1 at level " + std::to_string(j1) + ": " +
+                                             std::to_string(plan->o1_threads[j1]) +
+                                             " threads cannot hold the exported half spectrum (8 items each)");
     WST_HIP_CHECK(plan->ops->set_attrs());
     if (plan->rb > 0) {
         WST_HIP_CHECK(wstlaunch::wst_big_common_ops().set_attrs());
-        for (int r = 0; r < plan->rb; ++r) WST_HIP_CHECK(plan->big[r]->set_attrs());
+        for (int r = 0; r < plan->nst; ++r) {
+            WST_HIP_CHECK(plan->big_r[r]->set_attrs());
+            WST_HIP_CHECK(plan->big_c[r]->set_attrs());
+        }
     }
 
     *out = plan.release();
@@ -962,6 +999,16 @@ int wst_workspace_bytes(const wst_plan* plan, int64_t nbatch, size_t* bytes) {
     if (!plan || !bytes) return fail(WST_ERR_INVALID, "plan/bytes is NULL");
     if (nbatch < 0) return fail(WST_ERR_INVALID, "nbatch < 0");
     *bytes = static_cast<size_t>(nbatch) * plan->ws_plane;
+    return WST_OK;
+}
+
+int wst_internal_workspaces(const wst_plan* plan, int* count, size_t* bytes) {
+    if (!plan || !count || !bytes) return fail(WST_ERR_INVALID, "plan/count/bytes is NULL");
+    std::lock_guard<std::mutex> lk(plan->ws_mu);
+    *count = static_cast<int>(plan->ws_by_stream.size());
+    size_t b = 0;
+    for (const auto& kv : plan->ws_by_stream) b += kv.second.bytes;
+    *bytes = b;
     return WST_OK;
 }
 
@@ -1040,15 +1087,18 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
 }
 
 // The HBM-staged levels r < rb of one chunk (wst_staged.h): S0 + Xhat, then per staged j1 the
-// order-1 path (S1, U1hat) and its order-2 paths (staged while j2 < rb, then k_o2 on the global
-// spectrum).  Timing slots as the resident kernels: prep, o1 at j1, o2 at j1.
+// order-1 path (S1, U1hat) and its order-2 paths (staged while j2 < nst, then k_o2 on the global
+// spectrum).  Level r is m x n = (PM >> r) x (PN >> r): row passes run lines of n points (big_r),
+// column passes lines of m points (big_c).  Timing slots as the resident kernels: prep, o1 at j1,
+// o2 at j1.
 int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img0,
                   unsigned char* base, int64_t chunk, float* d_out, int pooled, hipStream_t stream,
                   LaunchTimer& timer) {
     using namespace wstbig;
     const wst::Geometry& g = plan->g;
     const DevParams& dp = plan->dp;
-    const int J = g.J, L = g.L, PM = g.PM, nq = (L + 1) / 2;
+    const int J = g.J, L = g.L, PM = g.PM, PN = g.PN, nq = (L + 1) / 2;
+    const int noms = plan->noms;
     const auto& cm = wstlaunch::wst_big_common_ops();
     float2* xhat = reinterpret_cast<float2*>(base);
     float2* tmp = reinterpret_cast<float2*>(base + plan->ws_tmp * chunk);
@@ -1060,114 +1110,122 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
     float* umean = mean + static_cast<size_t>(nimg) * kMeanParts;
     const dim3 tb(kBigThreads);
     auto gnat = [&](int r, int d) { return plan->d_lpn + plan->lpn_off[2 * r + d]; };
-    auto args = [&](int mode, int r) {
+    // row pass over level r: lines of PN >> r points, PM >> r rows
+    auto rargs = [&](int mode, int r) {
+        BigArgs a{};
+        a.mode = mode;
+        a.n = PN >> r;
+        a.nrows = PM >> r;
+        a.lvl = r;
+        a.rows = big_rows(mode, PM >> r);
+        a.L = L;
+        a.img0 = img0;
+        a.oms = noms;
+        return a;
+    };
+    // column pass over level r: lines of PM >> r points, `ncols` columns
+    auto cargs = [&](int mode, int r, int ncols) {
         BigArgs a{};
         a.mode = mode;
         a.n = PM >> r;
+        a.ncols = ncols;
         a.lvl = r;
-        a.rows = big_rows(mode, PM >> r);
-        a.ncols = PM >> r;
         a.L = L;
         a.img0 = img0;
-        a.oms = plan->oms;
+        a.oms = noms;
         return a;
     };
+    auto col_grid = [&](int ncols, int arrays) { return dim3((ncols + kColTile - 1) / kColTile, arrays); };
     int rc;
     // ---- S0 and Xhat (level 0) ----
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
     cm.mean(Launch{dim3(nimg, kMeanParts), tb, 0, stream}, dp, in, mean);
     {
-        BigArgs a = args(kRowPad, 0);
+        BigArgs a = rargs(kRowPad, 0);
         a.in = in;
         a.mean = mean;
         a.tpart = part;
         a.gnat = gnat(0, 1);
         a.dst = xhat;
-        plan->big[0]->rows(false, Launch{dim3(PM / a.rows, nimg), tb, plan->big_rows_lds[0], stream}, dp, a);
-        BigArgs c = args(kColStore, 0);
+        plan->big_r[0]->rows(false, Launch{dim3(PM / a.rows, nimg), tb, plan->big_rows_lds[0], stream}, dp, a);
+        BigArgs c = cargs(kColStore, 0, PN);
         c.dst = xhat;
-        plan->big[0]->cols(false, Launch{dim3((PM + kColTile - 1) / kColTile, nimg), tb, plan->big_cols_lds[0], stream},
-                           dp, c);
-        cm.final_(Launch{dim3(nimg), dim3(64), 0, stream}, dp, kFinalRows, 0, PM, plan->oms, part,
+        plan->big_c[0]->cols(false, Launch{col_grid(PN, nimg), tb, plan->big_cols_lds[0], stream}, dp, c);
+        cm.final_(Launch{dim3(nimg), dim3(64), 0, stream}, dp, kFinalRows, 0, PM, PN, noms, part,
                   gnat(0, 0), nullptr, nullptr, L, 0, 0, 0, 1, img0, d_out, pooled);
     }
     WST_HIP_CHECK(hipGetLastError());
     if ((rc = timer.end(stream, 0)) != WST_OK) return rc;
 
     for (int j1 = 0; j1 < plan->rb; ++j1) {
-        const int n1 = PM >> j1, hld = n1 / 2 + 1;
+        const int m1 = PM >> j1, n1 = PN >> j1, hld = n1 / 2 + 1;
         const bool do2 = g.max_order >= 2 && j1 < J - 1;
-        const auto* B1 = plan->big[j1];
         float2* hbig = do2 ? reinterpret_cast<float2*>(base + plan->ws_hbig[j1] * chunk) : nullptr;
         // ---- order 1: fold + inverse rows, inverse columns + |.| + low-pass partials, S1 ----
         if ((rc = timer.begin(stream)) != WST_OK) return rc;
-        BigArgs a = args(kRowFold1, j1);
+        BigArgs a = rargs(kRowFold1, j1);
         a.xhat = xhat;
         a.j1 = j1;
         a.dst = tmp;
-        B1->rows(true, Launch{dim3(n1 / a.rows, nimg * L), tb, plan->big_rows_lds[j1], stream}, dp, a);
-        BigArgs c = args(kColModLp, j1);
+        plan->big_r[j1]->rows(true, Launch{dim3(m1 / a.rows, nimg * L), tb, plan->big_rows_lds[j1], stream}, dp, a);
+        BigArgs c = cargs(kColModLp, j1, n1);
         c.dst = tmp;
         c.uout = do2 ? ureal : nullptr;
         c.vpart = part;
         c.csum = csum;
         c.scale = 1.f / (static_cast<float>(g.PM) * static_cast<float>(g.PN));
         c.gnat = gnat(j1, 0);
-        B1->cols(true, Launch{dim3((n1 + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds[j1], stream},
-                 dp, c);
-        cm.final_(Launch{dim3(nimg * L), dim3(64), 0, stream}, dp, kFinalCols, 1, n1, plan->oms, part,
+        plan->big_c[j1]->cols(true, Launch{col_grid(n1, nimg * L), tb, plan->big_cols_lds[j1], stream}, dp, c);
+        cm.final_(Launch{dim3(nimg * L), dim3(64), 0, stream}, dp, kFinalCols, 1, n1, m1, noms, part,
                   gnat(j1, 1), csum, do2 ? umean : nullptr, L, j1, 0, 0, 1, img0, d_out, pooled);
         if (do2) {
             // U1hat = fft2(U1 - mean) as half spectra (natural order) for the order-2 folds
-            BigArgs r2 = args(kRowReal2, j1);
+            BigArgs r2 = rargs(kRowReal2, j1);
             r2.ureal = ureal;
             r2.mean = umean;
             r2.dst = hbig;
-            B1->rows(false, Launch{dim3(n1 / r2.rows, nimg * L), tb, plan->big_rows_lds[j1], stream}, dp, r2);
-            BigArgs c2 = args(kColStore, j1);
-            c2.ncols = hld;
+            plan->big_r[j1]->rows(false, Launch{dim3(m1 / r2.rows, nimg * L), tb, plan->big_rows_lds[j1], stream},
+                                  dp, r2);
+            BigArgs c2 = cargs(kColStore, j1, hld);
             c2.dst = hbig;
-            B1->cols(false, Launch{dim3((hld + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds[j1], stream},
-                     dp, c2);
+            plan->big_c[j1]->cols(false, Launch{col_grid(hld, nimg * L), tb, plan->big_cols_lds[j1], stream}, dp, c2);
         }
         WST_HIP_CHECK(hipGetLastError());
         if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
         if (!do2) continue;
         // ---- order 2 from the staged U1hat ----
         if ((rc = timer.begin(stream)) != WST_OK) return rc;
-        for (int j2 = j1 + 1; j2 < plan->rb; ++j2) {
-            const int n2 = PM >> j2;
-            const auto* B2 = plan->big[j2];
+        for (int j2 = j1 + 1; j2 < plan->nst; ++j2) {
+            const int m2 = PM >> j2, n2 = PN >> j2;
             for (int l1 = 0; l1 < L; ++l1) {
-                BigArgs f = args(kRowFold2, j2);
+                BigArgs f = rargs(kRowFold2, j2);
                 f.hsrc = hbig;
                 f.n1 = n1;
                 f.l1 = l1;
                 f.j2 = j2;
                 f.psi2 = dp.psi2 + plan->psi2_off_host[(static_cast<size_t>(j2) * J + j1) * nq];
-                f.pstride = static_cast<long long>(n1) * n1;
+                f.pstride = static_cast<long long>(m1) * n1;
                 f.box = plan->d_box + plan->box_off_host[static_cast<size_t>(j2) * J + j1];
                 f.npair = nq;
                 f.npath = L;
                 f.dst = tmp;
                 size_t flds = plan->big_rows_lds[j2];
-                if (n1 == 2 * n2 && plan->fold_all_rows[j2] > 0) {
+                if (m1 == 2 * m2 && plan->fold_all_rows[j2] > 0) {
                     f.fold_all = 1;
                     f.rows = plan->fold_all_rows[j2];
                     flds = plan->fold_all_lds[j2];
                 }
-                B2->rows(true, Launch{dim3(n2 / f.rows, nimg), tb, flds, stream}, dp, f);
-                BigArgs m2 = args(kColModLp, j2);
-                m2.dst = tmp;
-                m2.vpart = part + static_cast<size_t>(l1) * nimg * L * n2 * plan->oms;
-                m2.csum = csum + static_cast<size_t>(l1) * nimg * L * n2;
-                m2.scale = 1.f / (static_cast<float>(n1) * static_cast<float>(n1));
-                m2.gnat = gnat(j2, 0);
-                B2->cols(true, Launch{dim3((n2 + kColTile - 1) / kColTile, nimg * L), tb, plan->big_cols_lds[j2], stream},
-                         dp, m2);
+                plan->big_r[j2]->rows(true, Launch{dim3(m2 / f.rows, nimg), tb, flds, stream}, dp, f);
+                BigArgs mc = cargs(kColModLp, j2, n2);
+                mc.dst = tmp;
+                mc.vpart = part + static_cast<size_t>(l1) * nimg * L * n2 * noms;
+                mc.csum = csum + static_cast<size_t>(l1) * nimg * L * n2;
+                mc.scale = 1.f / (static_cast<float>(m1) * static_cast<float>(n1));
+                mc.gnat = gnat(j2, 0);
+                plan->big_c[j2]->cols(true, Launch{col_grid(n2, nimg * L), tb, plan->big_cols_lds[j2], stream}, dp, mc);
             }
             // S2 of every theta1 in one launch (l1 = -1: blockIdx.y)
-            cm.final_(Launch{dim3(nimg * L, L), dim3(64), 0, stream}, dp, kFinalCols, 2, n2, plan->oms,
+            cm.final_(Launch{dim3(nimg * L, L), dim3(64), 0, stream}, dp, kFinalCols, 2, n2, m2, noms,
                       part, gnat(j2, 1), nullptr, nullptr, L, j1, -1, j2, L, img0, d_out, pooled);
         }
         const int j2f = plan->hg_j2first[j1];
@@ -1199,11 +1257,26 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
     void* ws = d_workspace;
     size_t wsb = workspace_bytes;
     std::unique_lock<std::mutex> ws_lock;   // held through the enqueue on an internal buffer
+    wst_plan::StreamWs* used = nullptr;
     if (!ws) {
-        // internal workspace of this stream: up to max_chunk planes per chunk
+        // internal workspace of this stream: up to max_chunk planes per chunk.  At most
+        // kMaxStreamWs streams keep one: a new stream evicts the least recently used buffer once
+        // that buffer's last work has completed (its event; valid even if its stream is gone)
         const int64_t want = std::min<int64_t>(nbatch, plan->max_chunk);
         ws_lock = std::unique_lock<std::mutex>(plan->ws_mu);
+        if (plan->ws_by_stream.find(stream) == plan->ws_by_stream.end() &&
+            plan->ws_by_stream.size() >= kMaxStreamWs) {
+            auto lru = plan->ws_by_stream.begin();
+            for (auto it = plan->ws_by_stream.begin(); it != plan->ws_by_stream.end(); ++it)
+                if (it->second.tick < lru->second.tick) lru = it;
+            if (lru->second.done) WST_HIP_CHECK(hipEventSynchronize(lru->second.done));
+            if (lru->second.ptr) (void)hipFree(lru->second.ptr);
+            if (lru->second.done) (void)hipEventDestroy(lru->second.done);
+            plan->ws_by_stream.erase(lru);
+        }
         wst_plan::StreamWs& sw = plan->ws_by_stream[stream];
+        sw.tick = ++plan->ws_tick;
+        used = &sw;
         if (sw.bytes < static_cast<size_t>(want) * plane_ws) {
             if (sw.ptr) {
                 // only this stream's calls use the buffer: once it drains, the buffer is idle
@@ -1217,6 +1290,7 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
         }
         ws = sw.ptr;
         wsb = sw.bytes;
+        if (!sw.done) WST_HIP_CHECK(hipEventCreateWithFlags(&sw.done, hipEventDisableTiming));
     }
     const int64_t cap = std::min<int64_t>(static_cast<int64_t>(wsb / plane_ws), plan->max_chunk);
     if (cap < 1) return fail(WST_ERR_INVALID, "workspace smaller than one plane's share");
@@ -1254,6 +1328,7 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
                                      timer)) != WST_OK)
                 return rc;
     }
+    if (used) WST_HIP_CHECK(hipEventRecord(used->done, stream));   // the buffer is busy until here
     return WST_OK;
 }
 

@@ -33,24 +33,28 @@ struct FamilyOps {
                int nimg, long long img0, const float2* hexp, float* out, int pooled, int j2first);
 };
 
-// HBM-staged passes of one big level size N (wst_staged.h), compiled per N (wst_staged.hip).
+// HBM-staged passes of one line length N (wst_staged.h), compiled per N (wst_staged.hip); n = 0:
+// the runtime-length instantiation.
 struct BigOps {
     int n;
     hipError_t (*set_attrs)();
     void (*rows)(bool inverse, const Launch&, const DevParams&, const wstbig::BigArgs&);
     void (*cols)(bool inverse, const Launch&, const DevParams&, const wstbig::BigArgs&);
 };
+// Compiled line lengths; every other length runs the N = 0 instantiation (generic DFT, n at run
+// time).  Keep in step with the Makefile's BIGNS.
 #define WST_BIG_SIZES(X) X(144) X(160) X(192) X(256) X(272) X(288) X(320) X(384) X(512)
 #define WST_BIG_GETTER(N) wst_big_ops_##N
 #define WST_DECLARE_BIG(N) const BigOps& WST_BIG_GETTER(N)();
 WST_BIG_SIZES(WST_DECLARE_BIG)
+WST_DECLARE_BIG(0)
 #undef WST_DECLARE_BIG
 
 // size-independent staged kernels (k_big_mean, k_big_final), in the N = 0 object
 struct BigCommonOps {
     hipError_t (*set_attrs)();
     void (*mean)(const Launch&, const DevParams&, const float* in, float* mean);
-    void (*final_)(const Launch&, const DevParams&, int fmode, int kind, int n, int oms,
+    void (*final_)(const Launch&, const DevParams&, int fmode, int kind, int n, int n_other, int oms,
                    const float* part, const float* G, const float* csum, float* mean_out, int L,
                    int j1, int l1, int j2, int npath, long long img0, float* out, int pooled);
 };

@@ -28,36 +28,41 @@ constexpr int kBigThreads = 256;
 constexpr int kColTile = 16;                    // columns per column-pass workgroup (128 B rows)
 constexpr int kMeanParts = 16;                  // k_big_mean partial sums per plane
 constexpr int kLoadBatch = 8;                   // global loads per thread in flight (tile loads)
+constexpr int kBigMaxO = 16;                    // output map side (oM, oN) the staged passes hold
 
 enum RowMode { kRowPad = 0, kRowReal2 = 1, kRowFold1 = 2, kRowFold2 = 3 };
 enum ColMode { kColStore = 0, kColModLp = 1 };
 enum FinalMode { kFinalRows = 0, kFinalCols = 1 };
 
-// Arguments of one staged launch (POD, by value).
+// Arguments of one staged launch (POD, by value).  A level's arrays are nrows x ncols (PM >> r by
+// PN >> r, or PN >> r / 2 + 1 columns for half spectra); a row pass transforms lines of n = ncols
+// points, a column pass lines of n = nrows points.  Kernels instantiated with N = 0 take n at run
+// time (generic DFT: sizes without a compiled FFT).
 struct BigArgs {
     int mode;
-    int n;                       // transform size of this level
+    int n;                       // line length of this pass
     int lvl;                     // level r (twiddles, tap matrices)
     int rows;                    // rows per workgroup (row pass)
-    int ncols;                   // columns of the array (n, or n/2 + 1 for half spectra)
+    int nrows;                   // row pass: rows of the array
+    int ncols;                   // column pass: columns of the array (its row stride)
     int L;
     long long img0;              // first plane of the chunk (output row)
     // kRowPad
     const float* in;
     const float* mean;           // kRowPad: plane sum partials (kMeanParts per plane);
                                  // kRowReal2: (plane, l1) U1 means
-    float* tpart;                // kRowPad: S0 row partials (n x oms per plane)
+    float* tpart;                // kRowPad: S0 row partials (nrows x oms per plane)
     // kRowFold1
     const float2* xhat;
     int j1;                      // kRowFold1: psi level-0 filters of scale j1; s = 2^j1
     // kRowReal2
-    const float* ureal;          // U1 (n x n per array)
+    const float* ureal;          // U1 (nrows x n per array)
     // kRowFold2
-    const float2* hsrc;          // half spectra at level j1 (n1 x (n1/2+1) per (plane, l1))
-    int n1, l1, j2;
+    const float2* hsrc;          // half spectra at level j1 ((nrows s) x (n1/2+1) per (plane, l1))
+    int n1, l1, j2;              // n1: row length at level j1 (= n s)
     const float2* psi2;          // pair 0 of (j2, j1) in the psi2 pool
-    long long pstride;           // n1^2 (pool stride between pairs)
-    const int* box;              // alias boxes of the pairs (s >= 4), stride n + n
+    long long pstride;           // (nrows s) n1 (pool stride between pairs)
+    const int* box;              // alias boxes of the pairs (s >= 4), stride nrows + n
     int npair, npath;            // pairs / paths per (plane, l1); one launch per l1, one
                                  // workgroup per (plane, row block) loops over the pairs
     int fold_all;                // kRowFold2, s = 2: every path of the block folded from one
@@ -65,40 +70,53 @@ struct BigArgs {
     // outputs
     float2* dst;
     float* uout;                 // kColModLp: U real (optional)
-    float* vpart;                // kColModLp: V[q][a] (n x oms per array)
-    float* csum;                 // kColModLp: column sums (n per array)
+    float* vpart;                // kColModLp: V[q][a] (ncols x oms per array)
+    float* csum;                 // kColModLp: column sums (ncols per array)
     float scale;                 // kColModLp
     const float* gnat;           // natural-order tap matrix: GN_0 (kRowPad) / GM_lvl (kColModLp)
     int oms;                     // row stride of the tap matrices and of tpart / vpart
 };
 
-__device__ __forceinline__ const float2* level_tw(const DevParams& p, int r) {
-    return p.tw + p.tw_off[2 * r];
+// twiddles exp(-2 pi i k / n) of level r: side 0 = M (column lines), 1 = N (row lines)
+__device__ __forceinline__ const float2* level_tw(const DevParams& p, int r, int side) {
+    return p.tw + p.tw_off[2 * r + side];
+}
+
+// n-point transforms along LDS lines: the compiled FFT for N > 0, the generic DFT for N = 0
+template <int N, bool INV, class Epi>
+__device__ __forceinline__ void big_fft(float2* A, const wstfft::Lines& g, int n, const float2* tw,
+                                        Epi& epi) {
+    if constexpr (N > 0)
+        wstfft::fft_lines<N, INV>(A, g, tw, epi);
+    else
+        wstdev::lds_dft_lines_generic(A, g, n, tw, INV, epi);
 }
 
 // --------------------------------------------------------------------------------------------
 // row pass
 // --------------------------------------------------------------------------------------------
-// LDS: twiddles (N) | lines (nlines x ld, ld = N | 1) | scratch.
+// LDS: twiddles (n) | lines (nlines x ld, ld = n | 1) | scratch.
 template <int N, bool INV>
 __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int ld = N | 1;
+    const int n = N > 0 ? N : a.n;
+    const int ld = n | 1;
+    const int m = a.nrows;
     float2* tw = reinterpret_cast<float2*>(smem);
-    float2* A = tw + N;
+    float2* A = tw + n;
     const int T = blockDim.x;
     const int arr = blockIdx.y;
     const int r0 = blockIdx.x * a.rows;
-    const float2* gtw = level_tw(p, a.lvl);
-    for (int i = threadIdx.x; i < N; i += T) tw[i] = gtw[i];
+    const float2* gtw = level_tw(p, a.lvl, 1);
+    for (int i = threadIdx.x; i < n; i += T) tw[i] = gtw[i];
     int nlines = a.rows;
 
     if (a.mode == kRowPad) {
         // arr = chunk-local plane; raw values first (S0 partials), then mean-centred
         const int inM = p.pre_pad ? p.PM : p.M, inN = p.pre_pad ? p.PN : p.N;
         const float* x = a.in + static_cast<long long>(arr) * inM * inN;
-        for (int i = threadIdx.x; i < a.rows * N; i += T) {
-            const int rr = i / N, q = i - (i / N) * N;
+        for (int i = threadIdx.x; i < a.rows * n; i += T) {
+            const int rr = i / n, q = i - (i / n) * n;
             const int u = r0 + rr;
             const int su = p.pre_pad ? u : wstdev::reflect_index(u - p.padTop, p.M);
             const int sv = p.pre_pad ? q : wstdev::reflect_index(q - p.padLeft, p.N);
@@ -111,54 +129,54 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
             const int o = w >> 3;
             const int rr = o / p.oN, c = o - (o / p.oN) * p.oN;
             float acc = 0.f;
-            for (int q = qc; q < N; q += 8) acc = fmaf(a.gnat[q * a.oms + c], A[rr * ld + q].x, acc);
+            for (int q = qc; q < n; q += 8) acc = fmaf(a.gnat[q * a.oms + c], A[rr * ld + q].x, acc);
             acc = wstdev::group_sum<8>(acc);
-            if (qc == 0) a.tpart[(static_cast<long long>(arr) * N + r0 + rr) * a.oms + c] = acc;
+            if (qc == 0) a.tpart[(static_cast<long long>(arr) * m + r0 + rr) * a.oms + c] = acc;
         }
         float msum = 0.f;   // plane mean from k_big_mean's partials, fixed order (deterministic)
         for (int k = 0; k < kMeanParts; ++k) msum += a.mean[arr * kMeanParts + k];
-        const float m = msum / (static_cast<float>(p.PM) * static_cast<float>(p.PN));
+        const float mu = msum / (static_cast<float>(p.PM) * static_cast<float>(p.PN));
         __syncthreads();
-        for (int i = threadIdx.x; i < a.rows * N; i += T) {
-            const int rr = i / N, q = i - (i / N) * N;
-            A[rr * ld + q].x -= m;
+        for (int i = threadIdx.x; i < a.rows * n; i += T) {
+            const int rr = i / n, q = i - (i / n) * n;
+            A[rr * ld + q].x -= mu;
         }
     } else if (a.mode == kRowReal2) {
         // arr = (plane, l1); rows r0 .. r0 + rows - 1 packed in pairs
         nlines = a.rows / 2;
-        const float* U = a.ureal + static_cast<long long>(arr) * N * N;
-        const float m = a.mean[arr];
-        for (int i0 = threadIdx.x; i0 < nlines * N; i0 += kLoadBatch * T) {
+        const float* U = a.ureal + static_cast<long long>(arr) * m * n;
+        const float mu = a.mean[arr];
+        for (int i0 = threadIdx.x; i0 < nlines * n; i0 += kLoadBatch * T) {
             float2 t2[kLoadBatch];
 #pragma unroll
             for (int k = 0; k < kLoadBatch; ++k) {
-                const int i = min(i0 + k * T, nlines * N - 1);
-                const int t = i / N, q = i - (i / N) * N;
+                const int i = min(i0 + k * T, nlines * n - 1);
+                const int t = i / n, q = i - (i / n) * n;
                 const int u = r0 + 2 * t;
-                t2[k] = make_float2(U[u * N + q], U[(u + 1) * N + q]);
+                t2[k] = make_float2(U[u * n + q], U[(u + 1) * n + q]);
             }
 #pragma unroll
             for (int k = 0; k < kLoadBatch; ++k) {
                 const int i = i0 + k * T;
-                const int t = i / N, q = i - (i / N) * N;
-                if (i < nlines * N) A[t * ld + q] = make_float2(t2[k].x - m, t2[k].y - m);
+                const int t = i / n, q = i - (i / n) * n;
+                if (i < nlines * n) A[t * ld + q] = make_float2(t2[k].x - mu, t2[k].y - mu);
             }
         }
     } else if (a.mode == kRowFold1) {
-        // arr = plane * L + l1: rows of fold_s(Xhat * psi0_{j1, l1}), Xhat is (N s) x (N s)
+        // arr = plane * L + l1: rows of fold_s(Xhat * psi0_{j1, l1}), Xhat is (m s) x (n s)
         const int plane = arr / a.L, l1 = arr - (arr / a.L) * a.L;
         const int s = 1 << a.j1;
-        const int PN = N * s;
-        const float2* X = a.xhat + static_cast<long long>(plane) * PN * PN;
+        const int PN = n * s;
+        const float2* X = a.xhat + static_cast<long long>(plane) * (m * s) * PN;
         const float* psi0 = p.psi + p.psi_off[(a.j1 * a.L + l1) * p.J + 0];
         if (s == 1) {
-            for (int i0 = threadIdx.x; i0 < a.rows * N; i0 += kLoadBatch * T) {
+            for (int i0 = threadIdx.x; i0 < a.rows * n; i0 += kLoadBatch * T) {
                 float2 xv[kLoadBatch];
                 float f[kLoadBatch];
 #pragma unroll
                 for (int k = 0; k < kLoadBatch; ++k) {
-                    const int i = min(i0 + k * T, a.rows * N - 1);
-                    const int rr = i / N, q = i - (i / N) * N;
+                    const int i = min(i0 + k * T, a.rows * n - 1);
+                    const int rr = i / n, q = i - (i / n) * n;
                     const long long idx = static_cast<long long>(r0 + rr) * PN + q;
                     f[k] = psi0[idx];
                     xv[k] = X[idx];
@@ -166,18 +184,18 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
 #pragma unroll
                 for (int k = 0; k < kLoadBatch; ++k) {
                     const int i = i0 + k * T;
-                    const int rr = i / N, q = i - (i / N) * N;
-                    if (i < a.rows * N) A[rr * ld + q] = make_float2(xv[k].x * f[k], xv[k].y * f[k]);
+                    const int rr = i / n, q = i - (i / n) * n;
+                    if (i < a.rows * n) A[rr * ld + q] = make_float2(xv[k].x * f[k], xv[k].y * f[k]);
                 }
             }
         } else
-        for (int i = threadIdx.x; i < a.rows * N; i += T) {
-            const int rr = i / N, q = i - (i / N) * N;
+        for (int i = threadIdx.x; i < a.rows * n; i += T) {
+            const int rr = i / n, q = i - (i / n) * n;
             const int u = r0 + rr;
             float2 acc = make_float2(0.f, 0.f);
             for (int ii = 0; ii < s; ++ii)
                 for (int jj = 0; jj < s; ++jj) {
-                    const long long idx = static_cast<long long>(u + ii * N) * PN + q + jj * N;
+                    const long long idx = static_cast<long long>(u + ii * m) * PN + q + jj * n;
                     const float f = psi0[idx];
                     const float2 xv = X[idx];
                     acc = make_float2(fmaf(xv.x, f, acc.x), fmaf(xv.y, f, acc.y));
@@ -185,9 +203,11 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
             A[rr * ld + q] = acc;
         }
     } else {  // kRowFold2: arr = plane (one l1 per launch); every pair in turn, 2 paths each
+        // level j1 is (m s) x n1, its real U1 held as half spectra of n1 / 2 + 1 columns
         const int n1 = a.n1, hld = n1 / 2 + 1, half = n1 / 2;
-        const int s = n1 / N, smask = s - 1;
-        const float2* H = a.hsrc + (static_cast<long long>(arr) * a.L + a.l1) * n1 * hld;
+        const int s = n1 / n, smask = s - 1;
+        const int m1 = m * s;
+        const float2* H = a.hsrc + (static_cast<long long>(arr) * a.L + a.l1) * m1 * hld;
         wstfft::EpiIdentity id;
         if (a.fold_all) {
             // s = 2 (dense): the four spectrum taps of an output bin are read once and serve every
@@ -195,18 +215,18 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
             // bytes at c5); path p of row rr lands on line p * rows + rr
             // KI bins per thread in flight: their 4 KI spectrum taps, then per pair 4 KI filter taps
             constexpr int KI = 2;
-            for (int i0 = threadIdx.x; i0 < a.rows * N; i0 += KI * T) {
+            for (int i0 = threadIdx.x; i0 < a.rows * n; i0 += KI * T) {
                 float2 h[KI][4];
                 int fo[KI][4];
 #pragma unroll
                 for (int k = 0; k < KI; ++k) {
-                    const int i = min(i0 + k * T, a.rows * N - 1);
-                    const int rr = i / N, v = i - (i / N) * N;
+                    const int i = min(i0 + k * T, a.rows * n - 1);
+                    const int rr = i / n, v = i - (i / n) * n;
                     const int u = r0 + rr;
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
-                        const int kr = u + (t >> 1) * N, kc = v + (t & 1) * N;
-                        const int krm = kr == 0 ? 0 : n1 - kr;
+                        const int kr = u + (t >> 1) * m, kc = v + (t & 1) * n;
+                        const int krm = kr == 0 ? 0 : m1 - kr;
                         const bool mir = kc > half;
                         h[k][t] = H[mir ? krm * hld + (n1 - kc) : kr * hld + kc];
                         h[k][t].y = mir ? -h[k][t].y : h[k][t].y;
@@ -223,8 +243,8 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
 #pragma unroll
                     for (int k = 0; k < KI; ++k) {
                         const int i = i0 + k * T;
-                        if (i >= a.rows * N) break;
-                        const int rr = i / N, v = i - (i / N) * N;
+                        if (i >= a.rows * n) break;
+                        const int rr = i / n, v = i - (i / n) * n;
                         float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
 #pragma unroll
                         for (int t = 0; t < 4; ++t) {
@@ -237,32 +257,32 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
                 }
             }
             __syncthreads();
-            wstfft::fft_lines<N, INV>(A, wstfft::Lines(1, 0, a.npath * a.rows, ld, 1), tw, id);
-            for (int i = threadIdx.x; i < a.npath * a.rows * N; i += T) {
-                const int line = i / N, q = i - (i / N) * N;
+            big_fft<N, INV>(A, wstfft::Lines(1, 0, a.npath * a.rows, ld, 1), n, tw, id);
+            for (int i = threadIdx.x; i < a.npath * a.rows * n; i += T) {
+                const int line = i / n, q = i - (i / n) * n;
                 const int path = line / a.rows, rr = line - path * a.rows;
-                float2* D = a.dst + (static_cast<long long>(arr) * a.npath + path) * N * N;
-                wstdev::stnt(D + (r0 + rr) * N + q, A[line * ld + q]);
+                float2* D = a.dst + (static_cast<long long>(arr) * a.npath + path) * m * n;
+                wstdev::stnt(D + (r0 + rr) * n + q, A[line * ld + q]);
             }
             return;
         }
         for (int pr = 0; pr < a.npair; ++pr) {
             const float2* ps = a.psi2 + pr * a.pstride;
-            const int* bx = a.box + pr * (N + N);
-            for (int i = threadIdx.x; i < a.rows * N; i += T) {
-                const int rr = i / N, v = i - (i / N) * N;
+            const int* bx = a.box + pr * (m + n);
+            for (int i = threadIdx.x; i < a.rows * n; i += T) {
+                const int rr = i / n, v = i - (i / n) * n;
                 const int u = r0 + rr;
                 int i0 = 0, ni = s, j0 = 0, nj = s;
                 if (bx && s >= 4) {
-                    const int rb = bx[u], cb = bx[N + v];
+                    const int rb = bx[u], cb = bx[m + v];
                     i0 = rb & 255; ni = rb >> 8; j0 = cb & 255; nj = cb >> 8;
                 }
                 float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
                 for (int ii = 0; ii < ni; ++ii) {
-                    const int kr = u + ((i0 + ii) & smask) * N;
-                    const int krm = kr == 0 ? 0 : n1 - kr;
+                    const int kr = u + ((i0 + ii) & smask) * m;
+                    const int krm = kr == 0 ? 0 : m1 - kr;
                     for (int jj = 0; jj < nj; ++jj) {
-                        const int kc = v + ((j0 + jj) & smask) * N;
+                        const int kc = v + ((j0 + jj) & smask) * n;
                         const bool mir = kc > half;
                         float2 h = H[mir ? krm * hld + (n1 - kc) : kr * hld + kc];
                         h.y = mir ? -h.y : h.y;
@@ -275,14 +295,14 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
                 A[(a.rows + rr) * ld + v] = a1;
             }
             __syncthreads();
-            wstfft::fft_lines<N, INV>(A, wstfft::Lines(1, 0, 2 * a.rows, ld, 1), tw, id);
+            big_fft<N, INV>(A, wstfft::Lines(1, 0, 2 * a.rows, ld, 1), n, tw, id);
             for (int b = 0; b < 2; ++b) {
                 const int path = 2 * pr + b;
                 if (path >= a.npath) break;
-                float2* D = a.dst + (static_cast<long long>(arr) * a.npath + path) * N * N;
-                for (int i = threadIdx.x; i < a.rows * N; i += T) {
-                    const int rr = i / N, q = i - (i / N) * N;
-                    wstdev::stnt(D + (r0 + rr) * N + q, A[(b * a.rows + rr) * ld + q]);
+                float2* D = a.dst + (static_cast<long long>(arr) * a.npath + path) * m * n;
+                for (int i = threadIdx.x; i < a.rows * n; i += T) {
+                    const int rr = i / n, q = i - (i / n) * n;
+                    wstdev::stnt(D + (r0 + rr) * n + q, A[(b * a.rows + rr) * ld + q]);
                 }
             }
             __syncthreads();
@@ -291,21 +311,21 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
     }
     __syncthreads();
     wstfft::EpiIdentity id;
-    wstfft::fft_lines<N, INV>(A, wstfft::Lines(1, 0, nlines, ld, 1), tw, id);
+    big_fft<N, INV>(A, wstfft::Lines(1, 0, nlines, ld, 1), n, tw, id);
 
     if (a.mode == kRowPad || a.mode == kRowFold1) {
-        float2* D = a.dst + static_cast<long long>(arr) * N * N;
-        for (int i = threadIdx.x; i < a.rows * N; i += T) {
-            const int rr = i / N, q = i - (i / N) * N;
-            wstdev::stnt(D + (r0 + rr) * N + q, A[rr * ld + q]);
+        float2* D = a.dst + static_cast<long long>(arr) * m * n;
+        for (int i = threadIdx.x; i < a.rows * n; i += T) {
+            const int rr = i / n, q = i - (i / n) * n;
+            wstdev::stnt(D + (r0 + rr) * n + q, A[rr * ld + q]);
         }
     } else if (a.mode == kRowReal2) {
-        constexpr int hld = N / 2 + 1;
-        float2* D = a.dst + static_cast<long long>(arr) * N * hld;
+        const int hld = n / 2 + 1;
+        float2* D = a.dst + static_cast<long long>(arr) * m * hld;
         for (int i = threadIdx.x; i < nlines * hld; i += T) {
             const int t = i / hld, q = i - (i / hld) * hld;
             const float2 z = A[t * ld + q];
-            const float2 zm = A[t * ld + (q == 0 ? 0 : N - q)];
+            const float2 zm = A[t * ld + (q == 0 ? 0 : n - q)];
             const int u = r0 + 2 * t;
             wstdev::stnt(D + u * hld + q, make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y)));
             wstdev::stnt(D + (u + 1) * hld + q, make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x)));
@@ -319,24 +339,25 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
 template <int N, bool INV>
 __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int ld = N | 1;
+    const int n = N > 0 ? N : a.n;
+    const int ld = n | 1;
     constexpr int C = kColTile;
     float2* tw = reinterpret_cast<float2*>(smem);
-    float2* A = tw + N;
+    float2* A = tw + n;
     const int T = blockDim.x;
     const int arr = blockIdx.y;
     const int c0 = blockIdx.x * C;
     const int nc = min(C, a.ncols - c0);
-    const float2* gtw = level_tw(p, a.lvl);
-    for (int i = threadIdx.x; i < N; i += T) tw[i] = gtw[i];
-    float2* src = a.dst + static_cast<long long>(arr) * N * a.ncols;
+    const float2* gtw = level_tw(p, a.lvl, 0);
+    for (int i = threadIdx.x; i < n; i += T) tw[i] = gtw[i];
+    float2* src = a.dst + static_cast<long long>(arr) * n * a.ncols;
     // kLoadBatch loads per thread in flight before their LDS stores (a load-store loop waits out
     // the HBM latency once per element: ~2.2 TB/s at c5)
-    for (int i0 = threadIdx.x; i0 < N * C; i0 += kLoadBatch * T) {
+    for (int i0 = threadIdx.x; i0 < n * C; i0 += kLoadBatch * T) {
         float2 t[kLoadBatch];
 #pragma unroll
         for (int k = 0; k < kLoadBatch; ++k) {
-            const int i = min(i0 + k * T, N * C - 1);
+            const int i = min(i0 + k * T, n * C - 1);
             const int u = i / C, c = min(i - (i / C) * C, nc - 1);
             t[k] = wstdev::ldnt(src + static_cast<long long>(u) * a.ncols + c0 + c);
         }
@@ -344,14 +365,14 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
         for (int k = 0; k < kLoadBatch; ++k) {
             const int i = i0 + k * T;
             const int u = i / C, c = i - (i / C) * C;
-            if (i < N * C && c < nc) A[c * ld + u] = t[k];
+            if (i < n * C && c < nc) A[c * ld + u] = t[k];
         }
     }
     __syncthreads();
     if (a.mode == kColStore) {
         wstfft::EpiIdentity id;
-        wstfft::fft_lines<N, INV>(A, wstfft::Lines(1, 0, nc, ld, 1), tw, id);
-        for (int i = threadIdx.x; i < N * C; i += T) {
+        big_fft<N, INV>(A, wstfft::Lines(1, 0, nc, ld, 1), n, tw, id);
+        for (int i = threadIdx.x; i < n * C; i += T) {
             const int u = i / C, c = i - (i / C) * C;
             if (c < nc) wstdev::stnt(src + static_cast<long long>(u) * a.ncols + c0 + c, A[c * ld + u]);
         }
@@ -359,42 +380,68 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
     }
     // kColModLp: |.| * scale in place (.x), then partials over the rows of each column
     wstdev::EpiModulus mod{a.scale, 0.f};
-    wstfft::fft_lines<N, INV>(A, wstfft::Lines(1, 0, nc, ld, 1), tw, mod);
+    big_fft<N, INV>(A, wstfft::Lines(1, 0, nc, ld, 1), n, tw, mod);
     if (a.uout) {
-        float* U = a.uout + static_cast<long long>(arr) * N * N;
-        for (int i = threadIdx.x; i < N * C; i += T) {
+        float* U = a.uout + static_cast<long long>(arr) * n * a.ncols;
+        for (int i = threadIdx.x; i < n * C; i += T) {
             const int u = i / C, c = i - (i / C) * C;
-            if (c < nc) U[static_cast<long long>(u) * N + c0 + c] = A[c * ld + u].x;
+            if (c < nc) U[static_cast<long long>(u) * a.ncols + c0 + c] = A[c * ld + u].x;
         }
     }
-    // V[q][a] = sum_p GMnat[p][a] m[p][q] (a < oM <= 8) and the column sum: the taps are staged in
-    // LDS after the column tile, one thread per (column, 16-row chunk) accumulates
+    // V[q][a] = sum_p GMnat[p][a] m[p][q] (a < oM <= kBigMaxO) and the column sum: the taps are
+    // staged in LDS after the column tile, one thread per (column, 16-row chunk) accumulates
     // every output of its rows, then the 16 chunks of a column are shuffle-reduced
     const int oms = a.oms;
-    float* G = reinterpret_cast<float*>(A + C * ld);   // N x oms taps after the column tile
-    for (int i = threadIdx.x; i < N * oms; i += T) G[i] = a.gnat[i];
+    float* G = reinterpret_cast<float*>(A + C * ld);   // n x oms taps after the column tile
+    for (int i = threadIdx.x; i < n * oms; i += T) G[i] = a.gnat[i];
     __syncthreads();
     constexpr int PC = 16;
+    if (p.oM <= 8) {
+        for (int w = threadIdx.x; w < nc * PC; w += T) {
+            const int pc = w & (PC - 1);
+            const int c = w / PC;
+            const float2* col = A + c * ld;
+            float acc[9];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) acc[k] = 0.f;
+            for (int u = pc; u < n; u += PC) {
+                const float mv = col[u].x;
+                const float* g = G + u * oms;
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (k < p.oM) acc[k] = fmaf(g[k], mv, acc[k]);
+                acc[8] += mv;
+            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) acc[k] = wstdev::group_sum<PC>(acc[k]);
+            if (pc == 0) {
+                for (int k = 0; k < p.oM; ++k) a.vpart[(static_cast<long long>(arr) * a.ncols + c0 + c) * oms + k] = acc[k];
+                a.csum[static_cast<long long>(arr) * a.ncols + c0 + c] = acc[8];
+            }
+        }
+        return;
+    }
+    // wide output maps (8 < oM <= kBigMaxO)
     for (int w = threadIdx.x; w < nc * PC; w += T) {
         const int pc = w & (PC - 1);
         const int c = w / PC;
         const float2* col = A + c * ld;
-        float acc[9];
+        float acc[kBigMaxO + 1];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) acc[k] = 0.f;
-        for (int u = pc; u < N; u += PC) {
-            const float m = col[u].x;
+        for (int k = 0; k <= kBigMaxO; ++k) acc[k] = 0.f;
+        for (int u = pc; u < n; u += PC) {
+            const float mv = col[u].x;
             const float* g = G + u * oms;
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (k < p.oM) acc[k] = fmaf(g[k], m, acc[k]);
-            acc[8] += m;
+            for (int k = 0; k < kBigMaxO; ++k)
+                if (k < p.oM) acc[k] = fmaf(g[k], mv, acc[k]);
+            acc[kBigMaxO] += mv;
         }
 #pragma unroll
-        for (int k = 0; k < 9; ++k) acc[k] = wstdev::group_sum<PC>(acc[k]);
+        for (int k = 0; k <= kBigMaxO; ++k) acc[k] = wstdev::group_sum<PC>(acc[k]);
         if (pc == 0) {
-            for (int k = 0; k < p.oM; ++k) a.vpart[(static_cast<long long>(arr) * N + c0 + c) * oms + k] = acc[k];
-            a.csum[static_cast<long long>(arr) * N + c0 + c] = acc[8];
+            for (int k = 0; k < p.oM; ++k) a.vpart[(static_cast<long long>(arr) * a.ncols + c0 + c) * oms + k] = acc[k];
+            a.csum[static_cast<long long>(arr) * a.ncols + c0 + c] = acc[kBigMaxO];
         }
     }
 }
@@ -426,20 +473,20 @@ __global__ void __launch_bounds__(kBigThreads) k_big_mean(DevParams p, const flo
 
 // --------------------------------------------------------------------------------------------
 // final low-pass contraction + emit, one workgroup per array
-//   kFinalRows: S[a][c] = sum_p G[p][a] T[p][c]   (T = S0 row partials, G = GMnat level 0)
-//   kFinalCols: S[a][c] = sum_q G[q][c] V[q][a]   (V = column partials, G = GNnat level lvl)
+//   kFinalRows: S[a][c] = sum_p G[p][a] T[p][c]   (T = S0 row partials, G = GMnat level 0; n rows)
+//   kFinalCols: S[a][c] = sum_q G[q][c] V[q][a]   (V = column partials, G = GNnat level lvl; n columns)
 // Coefficient of array `arr`: kind 0 -> k = 0 (plane = arr); 1 -> S1 (arr = plane*L + l1,
 // k = 1 + j1 L + l1); 2 -> S2 (arr = plane*npath + l2 for one l1, k = o2_base + (j2-j1-1) L + l2).
-// With `mean_out`, the U1 mean (sum of the column sums / n^2) of the array is stored too.
+// With `mean_out`, the U1 mean (sum of the column sums / (n n_other)) of the array is stored too.
 // --------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_big_final(DevParams p, int fmode, int kind, int n, int oms,
-                                                  const float* __restrict__ part,
+__global__ void __launch_bounds__(64) k_big_final(DevParams p, int fmode, int kind, int n, int n_other,
+                                                  int oms, const float* __restrict__ part,
                                                   const float* __restrict__ G,
                                                   const float* __restrict__ csum,
                                                   float* __restrict__ mean_out, int L, int j1,
                                                   int l1, int j2, int npath, long long img0,
                                                   float* __restrict__ out, int pooled) {
-    __shared__ float S[64];
+    __shared__ float S[kBigMaxO * kBigMaxO];
     __shared__ float red[16];
     const int arr = blockIdx.x;
     if (l1 < 0) {
@@ -468,7 +515,7 @@ __global__ void __launch_bounds__(64) k_big_final(DevParams p, int fmode, int ki
         float s = 0.f;
         for (int q = threadIdx.x; q < n; q += blockDim.x) s += csum[static_cast<long long>(arr) * n + q];
         s = wstdev::block_sum(s, red);
-        if (threadIdx.x == 0) mean_out[arr] = s / (static_cast<float>(n) * static_cast<float>(n));
+        if (threadIdx.x == 0) mean_out[arr] = s / (static_cast<float>(n) * static_cast<float>(n_other));
     }
     __syncthreads();
     long long plane;

@@ -1,17 +1,18 @@
-// HBM-staged kernels (wst_staged.h) of one big level size WST_BIG_N, set by the Makefile; the
-// object built with WST_BIG_N=0 carries the size-independent k_big_mean / k_big_final.
-#if defined(WST_BIG_N) && WST_BIG_N == 0
+// HBM-staged kernels (wst_staged.h) of one line length WST_BIG_N, set by the Makefile (0 = the
+// runtime-length instantiation); the object built with WST_BIG_COMMON carries the size-independent
+// k_big_mean / k_big_final.
+#ifdef WST_BIG_COMMON
 #define WST_BIG_COMMON_KERNELS
 #endif
 #include "wst_launch.h"
 
-#ifndef WST_BIG_N
-#error "WST_BIG_N must be defined (one object per big level size, 0 = common kernels)"
+#if !defined(WST_BIG_N) && !defined(WST_BIG_COMMON)
+#error "WST_BIG_N (one object per line length, 0 = runtime length) or WST_BIG_COMMON must be defined"
 #endif
 
 namespace wstlaunch {
 
-#if WST_BIG_N > 0
+#ifndef WST_BIG_COMMON
 namespace {
 
 constexpr int N = WST_BIG_N;
@@ -61,10 +62,10 @@ void mean(const Launch& q, const DevParams& dp, const float* in, float* m) {
     hipLaunchKernelGGL(wstbig::k_big_mean, q.grid, q.block, q.lds, q.st, dp, in, m);
 }
 
-void final_(const Launch& q, const DevParams& dp, int fmode, int kind, int n, int oms,
+void final_(const Launch& q, const DevParams& dp, int fmode, int kind, int n, int n_other, int oms,
             const float* part, const float* G, const float* csum, float* mean_out, int L, int j1,
             int l1, int j2, int npath, long long img0, float* out, int pooled) {
-    hipLaunchKernelGGL(wstbig::k_big_final, q.grid, q.block, q.lds, q.st, dp, fmode, kind, n, oms,
+    hipLaunchKernelGGL(wstbig::k_big_final, q.grid, q.block, q.lds, q.st, dp, fmode, kind, n, n_other, oms,
                        part, G, csum, mean_out, L, j1, l1, j2, npath, img0, out, pooled);
 }
 
