@@ -144,8 +144,20 @@ def test_staged_tall_plane_against_oracle():
     assert_parity(got, ref, TOL, "staged 128x256")
 
 
-def test_staged_wide_output_maps_are_unsupported():
+@pytest.mark.parametrize("M,N,J,L", [(200, 200, 3, 4),     # 216^2 padded, 25 x 25 maps
+                                     (640, 600, 2, 2)])    # 648 x 608, 160 x 150 maps (taps in L2)
+def test_staged_wide_output_maps_against_oracle(M, N, J, L):
+    """Output maps wider than the LDS-resident low-pass (oM > 8): the staged column pass runs its
+    outputs in groups of 16, reading the tap matrix from L2 when it does not fit beside the tile."""
+    x = np.random.default_rng(7).integers(0, 256, (1, M, N), dtype=np.uint8).astype(np.float32) / 255
+    ref = kr.Scattering2D(J=J, shape=(M, N), L=L)(x)
+    got = NpS(J=J, shape=(M, N), L=L)(x)
+    assert got.shape == ref.shape
+    assert_parity(got, ref, TOL, f"staged {M}x{N} J={J}")
+
+
+def test_staged_lines_beyond_lds_tiles_are_unsupported():
     with pytest.raises(_lib.WSTError) as e:
-        _lib.Plan(512, 512, 4, 8)                  # 544^2 padded, 32 x 32 output maps
+        _lib.Plan(2048, 2048, 2, 2)                # 2056^2 padded: 2056-point lines
     assert e.value.code == _lib.WST_ERR_UNSUPPORTED
-    assert "16 wide" in str(e.value)
+    assert "1204 points" in str(e.value)

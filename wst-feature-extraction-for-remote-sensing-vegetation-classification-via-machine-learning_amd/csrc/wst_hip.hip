@@ -188,6 +188,7 @@ struct wst_plan {
     std::vector<size_t> hg_lds;
     std::vector<int> hg_threads, hg_j2first;
     std::vector<size_t> big_rows_lds, big_cols_lds;   // per staged level (2 R lines / 16 columns)
+    std::vector<int> big_g_lds;                   // per staged level: kColModLp taps in LDS
     std::vector<int> fold_all_rows;               // per staged level: rows of the all-paths s = 2
     std::vector<size_t> fold_all_lds;             //   order-2 row pass (0: per-pair passes)
     std::vector<size_t> ws_hbig;                  // U1hat half spectra of staged j1 (per plane)
@@ -404,6 +405,17 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     wst::Geometry g;
     std::string err;
     if (!wst::make_geometry(M, N, J, L, max_order, g, err)) return fail(WST_ERR_INVALID, err);
+    // staged levels hold 2 kBigRows row lines / kColTile column lines of their level in LDS:
+    // checked before the (size-proportional) filter bank is built
+    for (int r = 0; r < J && std::max(g.PM, g.PN) >> r > wstbig::kBigMinN; ++r) {
+        const size_t nl = static_cast<size_t>(std::max(g.PM, g.PN) >> r);
+        const size_t lines = std::max<size_t>(2 * kBigRows, wstbig::kColTile);
+        if ((nl + lines * (nl | 1)) * sizeof(float2) > static_cast<size_t>(kMaxLds))
+            return fail(WST_ERR_UNSUPPORTED, "padded plane " + std::to_string(g.PM) + "x" + std::to_string(g.PN) +
+                                                 ": staged level " + std::to_string(r) + " lines of " +
+                                                 std::to_string(nl) + " points exceed the LDS line tiles " +
+                                                 "(160 KiB per CU; at most 1204 points)");
+    }
     wst::FilterBank fb;
     try {
         fb = wst::build_filter_bank(g, conv);
@@ -571,7 +583,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         }
     t.lpt_off.back() = static_cast<int>(lpt.size());
     // the same tap matrices in natural order (HBM-staged levels use natural-order transforms); row
-    // stride noms >= max(oM, oN) (the staged passes hold output maps up to kBigMaxO wide)
+    // stride noms >= max(oM, oN)
     const int noms = std::max(oms, (std::max(g.oM, g.oN) + 3) & ~3);
     std::vector<float> lpn;
     plan->lpn_off.assign(2 * static_cast<size_t>(J), 0);
@@ -719,12 +731,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     // leading levels too large for the LDS-resident kernels run HBM-staged (wst_staged.h)
     while (plan->rb < J && std::max(g.PM, g.PN) >> plan->rb > wstbig::kBigMinN) ++plan->rb;
     if (plan->rb > 0) {
-        if (std::max(g.oM, g.oN) > wstbig::kBigMaxO)
-            return fail(WST_ERR_UNSUPPORTED,
-                        "padded plane " + std::to_string(g.PM) + "x" + std::to_string(g.PN) +
-                            " needs HBM-staged levels, whose low-pass passes hold output maps up to " +
-                            std::to_string(wstbig::kBigMaxO) + " wide (here " + std::to_string(g.oM) +
-                            "x" + std::to_string(g.oN) + ")");
         // square compiled-family planes (sq) fold the order-2 levels from rb on out of the global
         // spectrum (k_o2 HG); any other plane runs every order-2 level of a staged j1 staged
         plan->nst = plan->sq ? plan->rb : J;
@@ -733,6 +739,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         plan->big_c.assign(nst, nullptr);
         plan->big_rows_lds.assign(nst, 0);
         plan->big_cols_lds.assign(nst, 0);
+        plan->big_g_lds.assign(nst, 1);
         for (int r = 0; r < nst; ++r) {
             const size_t nm = static_cast<size_t>(g.PM >> r), nn = static_cast<size_t>(g.PN >> r);
             plan->big_r[r] = big_ops(g.PN >> r);
@@ -740,6 +747,11 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
             plan->big_rows_lds[r] = (nn + 2 * kBigRows * (nn | 1)) * sizeof(float2);
             plan->big_cols_lds[r] = (nm + wstbig::kColTile * (nm | 1)) * sizeof(float2) +
                                     nm * static_cast<size_t>(noms) * sizeof(float);   // + tap matrix
+            if (plan->big_cols_lds[r] > static_cast<size_t>(kMaxLds) && g.oM > 8) {
+                // wide output maps: the tap matrix stays in L2
+                plan->big_g_lds[r] = 0;
+                plan->big_cols_lds[r] = (nm + wstbig::kColTile * (nm | 1)) * sizeof(float2);
+            }
             if (std::max(plan->big_rows_lds[r], plan->big_cols_lds[r]) > static_cast<size_t>(kMaxLds))
                 return fail(WST_ERR_UNSUPPORTED, "level " + std::to_string(r) + " (" + std::to_string(nm) + "x" +
                                                      std::to_string(nn) + ") exceeds the staged passes' " +
@@ -1133,9 +1145,11 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         a.L = L;
         a.img0 = img0;
         a.oms = noms;
+        a.g_lds = plan->big_g_lds[r];
         return a;
     };
     auto col_grid = [&](int ncols, int arrays) { return dim3((ncols + kColTile - 1) / kColTile, arrays); };
+    const size_t sbytes = static_cast<size_t>(g.oM) * g.oN * sizeof(float);   // k_big_final's S
     int rc;
     // ---- S0 and Xhat (level 0) ----
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
@@ -1151,7 +1165,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         BigArgs c = cargs(kColStore, 0, PN);
         c.dst = xhat;
         plan->big_c[0]->cols(false, Launch{col_grid(PN, nimg), tb, plan->big_cols_lds[0], stream}, dp, c);
-        cm.final_(Launch{dim3(nimg), dim3(64), 0, stream}, dp, kFinalRows, 0, PM, PN, noms, part,
+        cm.final_(Launch{dim3(nimg), dim3(64), sbytes, stream}, dp, kFinalRows, 0, PM, PN, noms, part,
                   gnat(0, 0), nullptr, nullptr, L, 0, 0, 0, 1, img0, d_out, pooled);
     }
     WST_HIP_CHECK(hipGetLastError());
@@ -1176,7 +1190,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         c.scale = 1.f / (static_cast<float>(g.PM) * static_cast<float>(g.PN));
         c.gnat = gnat(j1, 0);
         plan->big_c[j1]->cols(true, Launch{col_grid(n1, nimg * L), tb, plan->big_cols_lds[j1], stream}, dp, c);
-        cm.final_(Launch{dim3(nimg * L), dim3(64), 0, stream}, dp, kFinalCols, 1, n1, m1, noms, part,
+        cm.final_(Launch{dim3(nimg * L), dim3(64), sbytes, stream}, dp, kFinalCols, 1, n1, m1, noms, part,
                   gnat(j1, 1), csum, do2 ? umean : nullptr, L, j1, 0, 0, 1, img0, d_out, pooled);
         if (do2) {
             // U1hat = fft2(U1 - mean) as half spectra (natural order) for the order-2 folds
@@ -1225,7 +1239,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
                 plan->big_c[j2]->cols(true, Launch{col_grid(n2, nimg * L), tb, plan->big_cols_lds[j2], stream}, dp, mc);
             }
             // S2 of every theta1 in one launch (l1 = -1: blockIdx.y)
-            cm.final_(Launch{dim3(nimg * L, L), dim3(64), 0, stream}, dp, kFinalCols, 2, n2, m2, noms,
+            cm.final_(Launch{dim3(nimg * L, L), dim3(64), sbytes, stream}, dp, kFinalCols, 2, n2, m2, noms,
                       part, gnat(j2, 1), nullptr, nullptr, L, j1, -1, j2, L, img0, d_out, pooled);
         }
         const int j2f = plan->hg_j2first[j1];

@@ -28,7 +28,7 @@ constexpr int kBigThreads = 256;
 constexpr int kColTile = 16;                    // columns per column-pass workgroup (128 B rows)
 constexpr int kMeanParts = 16;                  // k_big_mean partial sums per plane
 constexpr int kLoadBatch = 8;                   // global loads per thread in flight (tile loads)
-constexpr int kBigMaxO = 16;                    // output map side (oM, oN) the staged passes hold
+constexpr int kBigOGroup = 16;                  // outputs per accumulation round of wide low-passes
 
 enum RowMode { kRowPad = 0, kRowReal2 = 1, kRowFold1 = 2, kRowFold2 = 3 };
 enum ColMode { kColStore = 0, kColModLp = 1 };
@@ -74,6 +74,7 @@ struct BigArgs {
     float* csum;                 // kColModLp: column sums (ncols per array)
     float scale;                 // kColModLp
     const float* gnat;           // natural-order tap matrix: GN_0 (kRowPad) / GM_lvl (kColModLp)
+    int g_lds;                   // kColModLp: tap matrix staged in LDS (0: read from L2)
     int oms;                     // row stride of the tap matrices and of tpart / vpart
 };
 
@@ -388,12 +389,16 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
             if (c < nc) U[static_cast<long long>(u) * a.ncols + c0 + c] = A[c * ld + u].x;
         }
     }
-    // V[q][a] = sum_p GMnat[p][a] m[p][q] (a < oM <= kBigMaxO) and the column sum: the taps are
-    // staged in LDS after the column tile, one thread per (column, 16-row chunk) accumulates
+    // V[q][a] = sum_p GMnat[p][a] m[p][q] (a < oM) and the column sum: the taps are staged in LDS
+    // after the column tile (when they fit), one thread per (column, 16-row chunk) accumulates
     // every output of its rows, then the 16 chunks of a column are shuffle-reduced
     const int oms = a.oms;
-    float* G = reinterpret_cast<float*>(A + C * ld);   // n x oms taps after the column tile
-    for (int i = threadIdx.x; i < n * oms; i += T) G[i] = a.gnat[i];
+    const float* G = a.gnat;
+    if (a.g_lds) {
+        float* Gl = reinterpret_cast<float*>(A + C * ld);   // n x oms taps after the column tile
+        for (int i = threadIdx.x; i < n * oms; i += T) Gl[i] = a.gnat[i];
+        G = Gl;
+    }
     __syncthreads();
     constexpr int PC = 16;
     if (p.oM <= 8) {
@@ -421,27 +426,30 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
         }
         return;
     }
-    // wide output maps (8 < oM <= kBigMaxO)
-    for (int w = threadIdx.x; w < nc * PC; w += T) {
-        const int pc = w & (PC - 1);
-        const int c = w / PC;
-        const float2* col = A + c * ld;
-        float acc[kBigMaxO + 1];
+    // wide output maps: kBigOGroup outputs per round over the column tile held in LDS
+    for (int a0 = 0; a0 < p.oM; a0 += kBigOGroup) {
+        for (int w = threadIdx.x; w < nc * PC; w += T) {
+            const int pc = w & (PC - 1);
+            const int c = w / PC;
+            const float2* col = A + c * ld;
+            float acc[kBigOGroup + 1];
 #pragma unroll
-        for (int k = 0; k <= kBigMaxO; ++k) acc[k] = 0.f;
-        for (int u = pc; u < n; u += PC) {
-            const float mv = col[u].x;
-            const float* g = G + u * oms;
+            for (int k = 0; k <= kBigOGroup; ++k) acc[k] = 0.f;
+            for (int u = pc; u < n; u += PC) {
+                const float mv = col[u].x;
+                const float* g = G + u * oms + a0;
 #pragma unroll
-            for (int k = 0; k < kBigMaxO; ++k)
-                if (k < p.oM) acc[k] = fmaf(g[k], mv, acc[k]);
-            acc[kBigMaxO] += mv;
-        }
+                for (int k = 0; k < kBigOGroup; ++k)
+                    if (a0 + k < p.oM) acc[k] = fmaf(g[k], mv, acc[k]);
+                acc[kBigOGroup] += mv;
+            }
 #pragma unroll
-        for (int k = 0; k <= kBigMaxO; ++k) acc[k] = wstdev::group_sum<PC>(acc[k]);
-        if (pc == 0) {
-            for (int k = 0; k < p.oM; ++k) a.vpart[(static_cast<long long>(arr) * a.ncols + c0 + c) * oms + k] = acc[k];
-            a.csum[static_cast<long long>(arr) * a.ncols + c0 + c] = acc[kBigMaxO];
+            for (int k = 0; k <= kBigOGroup; ++k) acc[k] = wstdev::group_sum<PC>(acc[k]);
+            if (pc == 0) {
+                for (int k = 0; k < kBigOGroup && a0 + k < p.oM; ++k)
+                    a.vpart[(static_cast<long long>(arr) * a.ncols + c0 + c) * oms + a0 + k] = acc[k];
+                if (a0 == 0) a.csum[static_cast<long long>(arr) * a.ncols + c0 + c] = acc[kBigOGroup];
+            }
         }
     }
 }
@@ -486,7 +494,7 @@ __global__ void __launch_bounds__(64) k_big_final(DevParams p, int fmode, int ki
                                                   float* __restrict__ mean_out, int L, int j1,
                                                   int l1, int j2, int npath, long long img0,
                                                   float* __restrict__ out, int pooled) {
-    __shared__ float S[kBigMaxO * kBigMaxO];
+    extern __shared__ float S[];   // oM x oN (dynamic)
     __shared__ float red[16];
     const int arr = blockIdx.x;
     if (l1 < 0) {

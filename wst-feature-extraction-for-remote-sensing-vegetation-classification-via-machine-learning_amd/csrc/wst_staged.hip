@@ -56,7 +56,12 @@ const BigOps& WST_BIG_EXPAND(WST_BIG_N)() {
 #else
 namespace {
 
-hipError_t common_attrs() { return hipSuccess; }
+// k_big_final holds the oM x oN map of an array in dynamic LDS (wide maps exceed the 64 KiB default)
+hipError_t common_attrs() {
+    // (less its static reduction scratch: the attribute bounds dynamic + static <= 160 KiB)
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(wstbig::k_big_final),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds - 256);
+}
 
 void mean(const Launch& q, const DevParams& dp, const float* in, float* m) {
     hipLaunchKernelGGL(wstbig::k_big_mean, q.grid, q.block, q.lds, q.st, dp, in, m);
