@@ -179,8 +179,8 @@ def pmc_file_config(name):
     return last if last in CONFIGS else "c2"
 
 
-def pmc_traffic(sha, kernel, config="c2"):
-    """HBM bytes per launch of `kernel` from committed rocprofv3 PMC passes of this exact build and
+def pmc_summary(sha, config="c2"):
+    """The newest committed rocprofv3 PMC summary (tools/pmc_hbm.py) of this exact build and
     geometry.  Kernel names repeat across geometries (c5's LDS-resident levels instantiate the same
     k_o2<3, 3, 136, ...> as c2), so only files of this config count; c3 / c4 run c2's kernels."""
     pdir = os.path.join(ROOT, "profiles")
@@ -193,14 +193,69 @@ def pmc_traffic(sha, kernel, config="c2"):
                 d = json.load(open(os.path.join(pdir, name)))
             except Exception:
                 continue
-            per = d.get("hbm_bytes_per_launch", {})
-            if sha not in (d.get("lib_sha"), d.get("src_sha")):
-                continue
-            # `kernel` is the template prefix "k_o2<3, 3, 136"; variants append ", SQ, HG>"
-            for kname, v in per.items():
-                if kname == kernel + ">" or kname.startswith(kernel + ","):
-                    return v
+            if sha in (d.get("lib_sha"), d.get("src_sha")):
+                return d
     return None
+
+
+def pmc_traffic(sha, kernel, config="c2"):
+    """HBM bytes per launch of `kernel` (template prefix "k_o2<3, 3, 136"; variants append
+    ", SQ, HG>") from the matching PMC summary."""
+    d = pmc_summary(sha, config)
+    if d is None:
+        return None
+    for kname, v in d.get("hbm_bytes_per_launch", {}).items():
+        if kname == kernel + ">" or kname.startswith(kernel + ","):
+            return v
+    return None
+
+
+BIG_SIZES = (96, 144, 160, 192, 256, 272, 288, 320, 384, 512)   # csrc/wst_launch.h WST_BIG_SIZES
+
+
+def staged_sequence(PM, PN, J, L, nst, max_order=2):
+    """[(timing slot, kernel)] of one chunk's HBM-staged levels, in launch order (a mirror of
+    staged_levels in csrc/wst_hip.hip; nst = rb for square compiled-family planes)."""
+    def big(kind, n, inv):
+        return f"k_big_{kind}<{n if n in BIG_SIZES else 0}, {'true' if inv else 'false'}>"
+    fm, fn = family(PM), family(PN)
+    rb = staged_levels(PM, PN, J)
+    seq = [("k_prep", "k_big_mean"), ("k_prep", big("rows", PN, False)),
+           ("k_prep", big("cols", PM, False)), ("k_prep", "k_big_final")]
+    for j1 in range(rb):
+        m1, n1 = PM >> j1, PN >> j1
+        do2 = max_order >= 2 and j1 < J - 1
+        o1, o2 = f"k_o1_j1={j1}", f"k_o2_j1={j1}"
+        seq += [(o1, big("rows", n1, True)), (o1, big("cols", m1, True)), (o1, "k_big_final")]
+        if not do2:
+            continue
+        seq += [(o1, big("rows", n1, False)), (o1, big("cols", m1, False))]
+        for j2 in range(j1 + 1, nst):
+            seq += [(o2, big("rows", PN >> j2, True)), (o2, big("cols", PM >> j2, True))] * L
+            seq.append((o2, "k_big_final"))
+        if max(j1 + 1, nst) < J:
+            seq.append((o2, f"k_o2<{fm}, {fn}, 136, 1, 1>"))
+    return seq
+
+
+def slot_traffic(summary, seq, slot):
+    """HBM bytes per chunk of a composite timing slot: the PMC dispatch sequence is matched
+    against the staged launch order `seq` chunk by chunk and the slot's kernels summed (mean over
+    the matched chunks); None when the recorded sequence does not follow `seq`."""
+    disp = (summary or {}).get("dispatch_seq")
+    if not disp:
+        return None
+    names = [n for n, _ in disp]
+    exp = [k for _, k in seq]
+    tot, nmatch, i = 0, 0, 0
+    while i + len(exp) <= len(names):
+        if names[i:i + len(exp)] == exp:
+            tot += sum(disp[i + k][1] for k, (sl, _) in enumerate(seq) if sl == slot)
+            nmatch += 1
+            i += len(exp)
+        else:
+            i += 1
+    return round(tot / nmatch) if nmatch else None
 
 
 # ------------------------------------------------------------------------------------------
@@ -603,13 +658,24 @@ def main():
     probes = None if args.no_probes else measure_probes(torch, lib, dev, stream)
     sha = src_sha()
     dname = rocprof_name(dom, plan.PM, plan.PN, J)
+    summary = pmc_summary(sha, args.config) or pmc_summary(lib_sha(), args.config)
+    rb = staged_levels(plan.PM, plan.PN, J)
+    if dom != "k_prep" and int(dom.split("=")[1]) >= rb:
+        traffic = pmc_traffic(sha, dname, args.config) or pmc_traffic(lib_sha(), dname, args.config)
+    else:   # composite slot of the staged levels: its kernels summed per chunk
+        nst = rb if (family(plan.PM) and plan.PM == plan.PN and plan.Mo <= 8) else J
+        traffic = slot_traffic(summary, staged_sequence(plan.PM, plan.PN, J, L, nst), dom)
+    avg_ms = kms[dom] / nchunks
     roofline = {
         "bound": "valu", "pipe": "fp32 VALU (LDS FFT butterflies; f32 MFMA only in the wide low-pass)",
         "kernel": f"{dom} ({dname}, ...>)", "achieved": round(achieved, 4), "peak": FP32_PEAK_TFLOPS,
         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
-        "traffic": pmc_traffic(sha, dname, args.config) or pmc_traffic(lib_sha(), dname, args.config),
+        "traffic": traffic,
+        # the same launch against the HBM roof: PMC bytes (FETCH_SIZE counts Infinity-Cache hits
+        # too) over the HIP-event duration, / the 8 TB/s spec peak
+        "hbm_frac": (round(traffic / (avg_ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 5) if traffic else None),
         "launches_per_step": nchunks,
-        "avg_launch_ms": round(kms[dom] / nchunks, 4),
+        "avg_launch_ms": round(avg_ms, 4),
         "alg_flop_per_launch": round(dom_flop / nchunks),
         "kernel_ms_per_step": {k: round(v, 4) for k, v in kms.items()},
         "all_kernels_tflops": round(planes * sum(flops.values()) / (sum(kms.values()) * 1e-3) / 1e12, 4),

@@ -44,6 +44,27 @@ def test_rocprof_names():
     assert "k_big_rows<192, 1>" in bench.rocprof_name("k_o1_j1=1", 384, 384, 6)
 
 
+def test_staged_slot_traffic_from_dispatch_sequence():
+    # c5 (384^2, J=6, L=12, square family 3: rb = nst = 2): one chunk = 41 staged launches
+    seq = bench.staged_sequence(384, 384, 6, 12, 2)
+    assert len(seq) == 4 + 5 + (2 * 12 + 1 + 1) + 5 + 1
+    assert seq[-1] == ("k_o2_j1=1", "k_o2<3, 3, 136, 1, 1>")
+    # a recorded run: two chunks, each followed by resident kernels, one byte count per launch
+    disp = []
+    for c in range(2):
+        disp += [[k, 10 if sl == "k_o2_j1=0" else 1] for sl, k in seq]
+        disp += [["k_o1<3, 3, 136, 1>", 7], ["k_o2<3, 3, 136, 1, 0>", 7]]
+    summ = {"dispatch_seq": disp}
+    assert bench.slot_traffic(summ, seq, "k_o2_j1=0") == 10 * (2 * 12 + 2)
+    assert bench.slot_traffic(summ, seq, "k_prep") == 4
+    assert bench.slot_traffic({"dispatch_seq": disp[5:]}, seq, "k_prep") == 4   # first chunk cut
+    assert bench.slot_traffic({}, seq, "k_prep") is None
+    # non-square / uncompiled sizes: every order-2 level staged, runtime-length passes named <0, ...>
+    seq2 = bench.staged_sequence(288, 160, 4, 8, 4)
+    assert ("k_o2_j1=0", "k_big_rows<0, true>") in seq2            # 80-point rows at level 1
+    assert not any(k.startswith("k_o2<") for _, k in seq2)
+
+
 def test_alg_flops_split_sums_to_the_cascade():
     # c2: 115.4 MFLOP per RGB patch
     f = bench.alg_flops_per_plane(96, 96, 4, 8)

@@ -108,6 +108,8 @@ struct LdsLayout {
                             // k_o2 that folds from HBM (HG = 1) instead of the row-transformed ones
     int nsplit;             // k_o2 HG: workgroups per (plane, theta1), batch b run by workgroup
                             // b % nsplit; one item's workgroups share an XCD (its L2 holds H)
+    int hgroup;             // k_o2 HG split: items per dispatch group of an XCD; within a group
+                            // the slots run batch-major (one batch of hgroup items, then the next)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -1589,10 +1591,16 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
         const int total = nimg * L;
         const int x = blockIdx.x;
         if ((total & 7) == 0) {
+            // hgroup items per group, batch-major inside it: concurrent workgroups of the XCD fold
+            // the same batch (its filter pairs stay in L2) for neighbouring items
             const int slot = x >> 3;
-            const int il = slot / nsplit;
-            ksplit = slot - il * nsplit;
-            item = (x & 7) * (total >> 3) + il;
+            const int nper = total >> 3;
+            const int G = max(1, lay.hgroup);
+            const int grp = slot / (nsplit * G);
+            const int rem = slot - grp * nsplit * G;
+            const int gc = min(G, nper - grp * G);
+            ksplit = rem / gc;
+            item = (x & 7) * nper + grp * G + (rem - ksplit * gc);
         } else {
             item = x / nsplit;
             ksplit = x - item * nsplit;
@@ -1711,13 +1719,18 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {
         // after a big level the paths start at the first LDS-resident level, which is the
         // family's single size of this class (> 136 / 2): compile-time sizes from there on
+        // (runtime sizes when a plan stages that level too and starts further down)
         constexpr int N2C = unique_level(FM, MAXN);
-        wstfft::static_for<0, 8>([&](auto kc) {
-            constexpr int k = decltype(kc)::value;
-            constexpr int NN2 = N2C >> k;
-            if constexpr ((NN2 << k) == N2C && NN2 >= 1)
-                if (j2first + k < J) level(j2first + k, NN2, NN2);
-        });
+        if ((PM >> j2first) == N2C) {
+            wstfft::static_for<0, 8>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int NN2 = N2C >> k;
+                if constexpr ((NN2 << k) == N2C && NN2 >= 1)
+                    if (j2first + k < J) level(j2first + k, NN2, NN2);
+            });
+        } else {
+            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2);
+        }
     } else {
         for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2);
     }

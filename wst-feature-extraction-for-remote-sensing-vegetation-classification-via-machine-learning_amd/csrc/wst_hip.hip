@@ -734,6 +734,8 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         // square compiled-family planes (sq) fold the order-2 levels from rb on out of the global
         // spectrum (k_o2 HG); any other plane runs every order-2 level of a staged j1 staged
         plan->nst = plan->sq ? plan->rb : J;
+        if (const char* e = diag_env("WST_NST"))   // staged order-2 levels below rb (A/B timing)
+            if (plan->sq) plan->nst = std::max(plan->rb, std::min(J, std::atoi(e)));
         const int nst = plan->nst;
         plan->big_r.assign(nst, nullptr);
         plan->big_c.assign(nst, nullptr);
@@ -836,6 +838,8 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
             nbatch += (L + pb - 1) / pb;
         }
         plan->hg_lay[j1].nsplit = std::min(nbatch, kHgSplit);
+        plan->hg_lay[j1].hgroup = 1;
+        if (const char* e = diag_env("WST_HG_GROUP")) plan->hg_lay[j1].hgroup = std::max(1, std::atoi(e));
         if (const char* e = diag_env("WST_HG_SPLIT")) {   // "n0,n1,...": per j1 (last one repeats)
             const char* q = e;
             for (int k = 0; k < j1 && std::strchr(q, ','); ++k) q = std::strchr(q, ',') + 1;

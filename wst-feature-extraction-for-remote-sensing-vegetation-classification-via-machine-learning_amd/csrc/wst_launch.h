@@ -43,7 +43,7 @@ struct BigOps {
 };
 // Compiled line lengths; every other length runs the N = 0 instantiation (generic DFT, n at run
 // time).  Keep in step with the Makefile's BIGNS.
-#define WST_BIG_SIZES(X) X(144) X(160) X(192) X(256) X(272) X(288) X(320) X(384) X(512)
+#define WST_BIG_SIZES(X) X(96) X(144) X(160) X(192) X(256) X(272) X(288) X(320) X(384) X(512)
 #define WST_BIG_GETTER(N) wst_big_ops_##N
 #define WST_DECLARE_BIG(N) const BigOps& WST_BIG_GETTER(N)();
 WST_BIG_SIZES(WST_DECLARE_BIG)
