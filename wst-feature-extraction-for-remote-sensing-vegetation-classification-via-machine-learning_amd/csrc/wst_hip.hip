@@ -319,7 +319,8 @@ size_t layout(LdsLayout& lay, size_t data_a, size_t data_b, const TableOffsets& 
 constexpr size_t kMaxStreamWs = 4;   // streams that keep an internal workspace per plan
 
 // paths per order-2 batch at level j2 (mirrors k_o2)
-constexpr int kHgSplit = 3;   // k_o2 HG workgroups per (plane, theta1)
+constexpr int kHgSplit = 4;   // k_o2 HG workgroups per (plane, theta1)
+constexpr int kHgGroup = 16;  // k_o2 HG items per batch-major dispatch group of an XCD
 
 int paths_per_batch(size_t bcap, size_t pslot, int L) {
     const int nq = (L + 1) / 2;
@@ -831,14 +832,17 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         // the batches of an item split over kHgSplit workgroups on one XCD: they fold from the same
         // H, which that XCD's L2 then serves (one workgroup per item re-reads it from HBM once per
         // batch; one workgroup per batch repeats the table set-up 10x at c5: measured 1 / 3 / 6 /
-        // 10 workgroups per item, c5 29.66 / 29.08 / 29.35 / 30.09 ms)
+        // 10 workgroups per item, c5 29.66 / 29.08 / 29.35 / 30.09 ms).  Dispatch slots run
+        // batch-major over groups of kHgGroup items, so the workgroups an XCD runs together fold the
+        // same filter pairs (c5 split x group, ms/step: 3 x 1 26.29, 5 x 16 26.10, 4 x 16 25.89,
+        // 6 x 8 26.16; HG fetch per chunk at j1 = 0 / 1: 4.04 / 0.54 GB -> 2.46 / 0.27 GB at 4 x 16)
         int nbatch = 0;
         for (int j2 = j2f; j2 < J; ++j2) {
             const int pb = paths_per_batch(bcap, pslot(j2), L);
             nbatch += (L + pb - 1) / pb;
         }
         plan->hg_lay[j1].nsplit = std::min(nbatch, kHgSplit);
-        plan->hg_lay[j1].hgroup = 1;
+        plan->hg_lay[j1].hgroup = kHgGroup;
         if (const char* e = diag_env("WST_HG_GROUP")) plan->hg_lay[j1].hgroup = std::max(1, std::atoi(e));
         if (const char* e = diag_env("WST_HG_SPLIT")) {   // "n0,n1,...": per j1 (last one repeats)
             const char* q = e;
