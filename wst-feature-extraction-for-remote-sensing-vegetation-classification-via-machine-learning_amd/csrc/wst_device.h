@@ -1571,18 +1571,23 @@ constexpr int o2_min_waves(int cap) { return cap == 48 ? 6 : cap == 24 ? 5 : 1; 
 // HG = 1: the level-j1 spectrum is a big (HBM-staged, wst_staged.h) level: `hexp` holds the
 // fully transformed half spectra in natural order, the fold reads them from HBM (no LDS copy,
 // no column FFT) and the paths start at j2first (the first LDS-resident level).
-// k_o2 body; OC > 0: the output maps are OC x OC (compile-time; the common 4 x 4 of the headline)
+// k_o2 body; OC > 0: the output maps are OC x OC (compile-time; the common 4 x 4 of the headline).
+// LC > 0 (even): L = LC at compile time; the first order-2 level (j2 = j1 + 1) runs in batches of
+// two paths (one filter pair; a smaller batch than the layout allows is always valid) and every
+// deeper level in one batch of all LC paths (the layout's B holds LC paths of level j1 + 2, so of
+// every level below it), so each batch shape -- paths, pairs, lines, loop bounds and divisors --
+// folds at compile time.
 #ifndef WST_HG_R
 #define WST_HG_R (HG ? 2 : 1)
 #endif
-template <int FM, int FN, int MAXN, int SQ, int HG, int OC>
+template <int FM, int FN, int MAXN, int SQ, int HG, int OC, int LC = 0>
 __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& p,
                                           const LdsLayout& lay, int j1, int nimg, long long img0,
                                           const float2* __restrict__ hexp, float* __restrict__ out,
                                           int pooled, int j2first) {
     const int oM = OC ? OC : p.oM, oN = OC ? OC : p.oN;
     const int oms = OC ? 4 : lay.oms;
-    const int J = p.J, L = p.L;
+    const int J = p.J, L = LC ? LC : p.L;
     const int nsplit = HG ? max(1, lay.nsplit) : 1;
     int item, ksplit = 0;
     if (nsplit > 1) {
@@ -1645,19 +1650,21 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     const int kbase = p.o2_base[j1 * L + l1];
     const int nq = (L + 1) >> 1;
     int bctr = 0;   // batch counter (split HG launches)
-    // every batch of paths of level j2 (sizes nM2 x nN2)
-    auto level = [&](int j2, int nM2, int nN2) __attribute__((always_inline)) {
+    // every batch of paths of level j2 (sizes nM2 x nN2); PB > 0: compile-time paths per batch
+    auto level = [&](int j2, int nM2, int nN2, auto pbc) __attribute__((always_inline)) {
+        constexpr int PB = decltype(pbc)::value;
         const int ld2 = odd_ld(nN2);
         const int pslot = nM2 * ld2;
         const int s2 = 1 << (j2 - j1);
         int pb = lay.bcap / pslot;                 // paths per batch (multiple of 2)
-        pb = max(2, min(pb & ~1, 2 * nq));
+        pb = PB ? PB : max(2, min(pb & ~1, 2 * nq));
+#pragma unroll 1
         for (int l2a = 0; l2a < L; l2a += pb) {
             if (nsplit > 1) {
                 const int bi = bctr++;
                 if (bi % nsplit != ksplit) continue;
             }
-            const int npath = min(pb, L - l2a);
+            const int npath = (PB > 0 && LC % (PB > 0 ? PB : 1) == 0) ? PB : min(pb, L - l2a);
             const int npair = (npath + 1) >> 1;
             const float2* ps = p.psi2 + p.psi2_off[(j2 * J + j1) * nq + (l2a >> 1)];
             const long long pstride = static_cast<long long>(n1);
@@ -1714,7 +1721,8 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             constexpr int k = decltype(kc)::value;
             constexpr int NN2 = N1C >> k;
             if constexpr ((NN2 << k) == N1C && NN2 >= 1)
-                if (j1 + k < J && j1 + k >= j2first) level(j1 + k, NN2, NN2);
+                if (j1 + k < J && j1 + k >= j2first)
+                    level(j1 + k, NN2, NN2, std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{});
         });
     } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {
         // after a big level the paths start at the first LDS-resident level, which is the
@@ -1726,13 +1734,13 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                 constexpr int k = decltype(kc)::value;
                 constexpr int NN2 = N2C >> k;
                 if constexpr ((NN2 << k) == N2C && NN2 >= 1)
-                    if (j2first + k < J) level(j2first + k, NN2, NN2);
+                    if (j2first + k < J) level(j2first + k, NN2, NN2, std::integral_constant<int, 0>{});
             });
         } else {
-            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2);
+            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{});
         }
     } else {
-        for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2);
+        for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{});
     }
 }
 
@@ -1744,6 +1752,14 @@ __global__ void __launch_bounds__((HG && !SQ) ? WST_O2X_BOUND : 1024, o2_min_wav
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if constexpr (SQ) {
         if (p.oM == 4 && p.oN == 4 && lay.oms == 4) {
+#ifndef WST_NO_LC8
+            if constexpr (!HG && unique_level(FM, MAXN) > 0) {
+                if (p.L == 8) {
+                    k_o2_body<FM, FN, MAXN, SQ, HG, 4, 8>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
+                    return;
+                }
+            }
+#endif
             k_o2_body<FM, FN, MAXN, SQ, HG, 4>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
             return;
         }
