@@ -1739,6 +1739,30 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
         } else {
             for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{});
         }
+    } else if constexpr (!SQ && HG == 1 && FM == FN && FM > 0) {
+        // exported-spectrum k_o2 (f3 / c1): a square level of one of the family's sizes in this
+        // class runs with compile-time path sizes (and, with LC, compile-time batch shapes)
+        bool done = false;
+        if (PM == PN && j2first == j1 + 1) {
+            wstfft::static_for<0, 8>([&](auto mc) {
+                constexpr int N1X = FM << decltype(mc)::value;
+                if constexpr (N1X <= MAXN && N1X > prev_cap(MAXN)) {
+                    if (!done && (PM >> j1) == N1X) {
+                        done = true;
+                        wstfft::static_for<1, 8>([&](auto kc) {
+                            constexpr int k = decltype(kc)::value;
+                            constexpr int NN2 = N1X >> k;
+                            if constexpr ((NN2 << k) == N1X && NN2 >= 1)
+                                if (j1 + k < J)
+                                    level(j1 + k, NN2, NN2,
+                                          std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{});
+                        });
+                    }
+                }
+            });
+        }
+        if (!done)
+            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{});
     } else {
         for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{});
     }
@@ -1764,6 +1788,14 @@ __global__ void __launch_bounds__((HG && !SQ) ? WST_O2X_BOUND : 1024, o2_min_wav
             return;
         }
     }
+#ifndef WST_NO_LC8
+    if constexpr (!SQ && HG && FM == FN && FM > 0) {
+        if (p.L == 8) {
+            k_o2_body<FM, FN, MAXN, SQ, HG, 0, 8>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
+            return;
+        }
+    }
+#endif
     k_o2_body<FM, FN, MAXN, SQ, HG, 0>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
 }
 
