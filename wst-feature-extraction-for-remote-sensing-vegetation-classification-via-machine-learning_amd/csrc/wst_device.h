@@ -1427,8 +1427,9 @@ constexpr int o1_min_waves(int cap, int fm, int fn) {
 // ------------------------------------------------------------------------------------------
 // k_o1: one workgroup per (plane, theta1) at fixed j1 -- order 1 + half-spectrum export
 // ------------------------------------------------------------------------------------------
-// k_o1 body; OC > 0: the output maps are OC x OC (compile-time; the common 4 x 4 of the headline)
-template <int FM, int FN, int MAXN, int SQ, int OC>
+// k_o1 body; OC > 0: the output maps are OC x OC (compile-time; the common 4 x 4 of the headline);
+// N1T > 0: the (square) level size at compile time
+template <int FM, int FN, int MAXN, int SQ, int OC, int N1T = 0>
 __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& p,
                                           const LdsLayout& lay, int j1, int nimg, long long img0,
                                           const float2* __restrict__ xhat, float2* __restrict__ hexp,
@@ -1441,7 +1442,7 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     const int l1 = item - local * L;
     const long long img = img0 + local;
     const int PM = p.PM, PN = p.PN;
-    constexpr int N1C = SQ ? unique_level(FM, MAXN) : 0;
+    constexpr int N1C = N1T ? N1T : SQ ? unique_level(FM, MAXN) : 0;
     const int nM1 = N1C ? N1C : PM >> j1, nN1 = N1C ? N1C : PN >> j1;
     const int n1 = nM1 * nN1, ld1 = odd_ld(nN1);
     const bool do2 = (p.max_order >= 2) && (j1 < J - 1);
@@ -1558,6 +1559,24 @@ __global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevPara
             return;
         }
     }
+#ifndef WST_NO_N1T
+    if constexpr (!SQ && FM == FN && FM > 0) {
+        // square levels of the family's sizes in this class: compile-time level size (f3 / c1)
+        if (p.PM == p.PN) {
+            bool done = false;
+            wstfft::static_for<0, 8>([&](auto mc) {
+                constexpr int N1X = FM << decltype(mc)::value;
+                if constexpr (N1X <= MAXN && N1X > prev_cap(MAXN)) {
+                    if (!done && (p.PM >> j1) == N1X) {
+                        done = true;
+                        k_o1_body<FM, FN, MAXN, SQ, 0, N1X>(smem, p, lay, j1, nimg, img0, xhat, hexp, out, pooled);
+                    }
+                }
+            });
+            if (done) return;
+        }
+    }
+#endif
     k_o1_body<FM, FN, MAXN, SQ, 0>(smem, p, lay, j1, nimg, img0, xhat, hexp, out, pooled);
 }
 
