@@ -963,6 +963,8 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         // c1 1.50 -> 1.62): H is 21-75 KB, not the 0.15-0.6 MB of a staged level
         plan->o2x_lay[j1].nsplit = 1;
         if (const char* e = diag_env("WST_O2X_SPLIT")) plan->o2x_lay[j1].nsplit = std::max(1, std::atoi(e));
+        plan->o2x_lay[j1].hgroup = 1;
+        if (const char* e = diag_env("WST_O2X_GROUP")) plan->o2x_lay[j1].hgroup = std::max(1, std::atoi(e));
     }
     for (int j1 = plan->rb; j1 < J; ++j1) {
         plan->o1_threads[j1] = fill_cu(plan->o1_threads[j1], plan->o1_lds[j1]);
