@@ -1394,20 +1394,27 @@ __device__ __forceinline__ void prep_body(unsigned char* smem, const DevParams& 
     for (GridIter it(PN); it.u < PM; it.next()) dst[it.u * PN + it.v] = A[it.u * ld + it.v];
 }
 
-// One workgroup per plane.  Square planes at the family's single 96^2-class size (unique_level)
-// run with compile-time sizes.
+// One workgroup per plane.  Square planes of the family's sizes in (48, 136] run with compile-time
+// sizes.
 template <int FM, int FN>
 __global__ void __launch_bounds__(1024) k_prep(DevParams p, LdsLayout lay,
                                                const float* __restrict__ in, long long img0,
                                                float2* __restrict__ xhat, float* __restrict__ out,
                                                int pooled) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int PC = FM == FN ? unique_level(FM, 136) : 0;
-    if constexpr (PC > 0) {
-        if (p.PM == PC && p.PN == PC) {
-            prep_body<FM, FN, PC>(smem, p, lay, in, img0, xhat, out, pooled);
-            return;
-        }
+    if constexpr (FM == FN && FM > 0) {
+        // square planes of the family's sizes in (48, 136]: compile-time size
+        bool done = false;
+        wstfft::static_for<0, 8>([&](auto mc) {
+            constexpr int PC = FM << decltype(mc)::value;
+            if constexpr (PC > 48 && PC <= 136) {
+                if (!done && p.PM == PC && p.PN == PC) {
+                    done = true;
+                    prep_body<FM, FN, PC>(smem, p, lay, in, img0, xhat, out, pooled);
+                }
+            }
+        });
+        if (done) return;
     }
     prep_body<FM, FN, 0>(smem, p, lay, in, img0, xhat, out, pooled);
 }
