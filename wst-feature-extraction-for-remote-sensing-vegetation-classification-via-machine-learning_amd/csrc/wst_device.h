@@ -75,8 +75,6 @@ struct DevParams {
     const int* o2_base;           // first order-2 coefficient of each n1 = j1*L + l1
     const float2* psi2;           // order-2 filters, 2 consecutive l2 interleaved per bin
     const long long* psi2_off;    // [(j2*J + r)*ceil(L/2) + q] -> level r of l2 in {2q, 2q+1}
-    const float* psi2s;           // single-path order-2 filters of the mirror-symmetric s = 2 levels
-    const long long* psi2s_off;   // [(j2*J + r)*L + l] -> level r of psi_{j2, l}; -1: no mirror fold
     const int* box;               // order-2 alias boxes: per pair, nM2 row then nN2 column
                                   // entries (first alias | count << 8); pairs of one (j2, r)
                                   // contiguous, stride box_stride[j2]
@@ -716,7 +714,7 @@ template <int NN>
 __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, int ld,
                                            const float2* tw, const float* GM, const float* GN,
                                            int oms, int oM, int oN, float scale, float* S,
-                                           float* outd, int kstep = 1) {
+                                           float* outd) {
     using F = wstfft::LineFFT<NN, true>;
     constexpr bool single = (F::N2 == 1);
     constexpr int RU = single ? NN : F::N2;  // rows per unit
@@ -822,7 +820,7 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
         }
         acc = group_sum<QC>(acc);
         if (qc == 0) {
-            if (outd) __builtin_nontemporal_store(acc, outd + o + b * (kstep - 1) * (oM * oN));
+            if (outd) __builtin_nontemporal_store(acc, outd + o);
             else S[o] = acc;
         }
     }
@@ -833,16 +831,16 @@ template <int FAM, int K, int HI>
 __device__ __forceinline__ void family_cols_modlp(float2* U, int nb, int bs, int rows, int cols,
                                                   int ld, const float2* tw, const float* GM,
                                                   const float* GN, int oms, int oM, int oN,
-                                                  float scale, float* S, float* outd, int kstep = 1) {
+                                                  float scale, float* S, float* outd) {
     constexpr int NN = FAM << K;
     if constexpr (FAM > 0 && NN <= HI && NN <= wstfft::kMaxFamilyN) {
         if constexpr (NN >= 2) {
             if (rows == NN) {
-                cols_modlp<NN>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd, kstep);
+                cols_modlp<NN>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
                 return;
             }
         }
-        family_cols_modlp<FAM, K + 1, HI>(U, nb, bs, rows, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd, kstep);
+        family_cols_modlp<FAM, K + 1, HI>(U, nb, bs, rows, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
     }
 }
 
@@ -852,10 +850,8 @@ __device__ __forceinline__ void family_cols_modlp(float2* U, int nb, int bs, int
 // reference's 128^2 J=2 geometry holds 1024 values: 11.4 -> 3.2 ms per 256 RGB patches).
 // Called by every thread of the block (whole waves).
 // S addressing as lds_lowpass_mfma (s_bs < 0: contiguous maps).
-// kstep: coefficient distance between consecutive arrays of the batch (1: consecutive theta2)
 __device__ __forceinline__ void emit(const float* S, int nb, int k0, long long img, int K, int oM,
-                                     int oN, float* out, int pooled, int s_bs = -1, int s_es = 1,
-                                     int kstep = 1) {
+                                     int oN, float* out, int pooled, int s_bs = -1, int s_es = 1) {
     const int npix = oM * oN;
     if (s_bs < 0) s_bs = npix;
     if (!pooled) {
@@ -864,7 +860,7 @@ __device__ __forceinline__ void emit(const float* S, int nb, int k0, long long i
         for (int o = threadIdx.x; o < tot; o += blockDim.x) {
             const int b = dpix.div(o);
             const int i = o - b * npix;
-            out[(img * K + k0 + b * kstep) * npix + i] = S[b * s_bs + i * s_es];
+            out[(img * K + k0 + b) * npix + i] = S[b * s_bs + i * s_es];
         }
     } else if (npix <= 32) {   // small maps (the headline's 4 x 4): one thread per map
         for (int b = threadIdx.x; b < nb; b += blockDim.x) {
@@ -877,8 +873,8 @@ __device__ __forceinline__ void emit(const float* S, int nb, int k0, long long i
                 const float d = v[i * s_es] - m;
                 q = fmaf(d, d, q);
             }
-            out[img * 2 * K + k0 + b * kstep] = m;
-            out[img * 2 * K + K + k0 + b * kstep] = sqrtf(q / npix);
+            out[img * 2 * K + k0 + b] = m;
+            out[img * 2 * K + K + k0 + b] = sqrtf(q / npix);
         }
     } else {
         const int lane = threadIdx.x & 63, nw = (blockDim.x + 63) >> 6;
@@ -894,8 +890,8 @@ __device__ __forceinline__ void emit(const float* S, int nb, int k0, long long i
             }
             q = group_sum<64>(q);
             if (lane == 0) {
-                out[img * 2 * K + k0 + b * kstep] = m;
-                out[img * 2 * K + K + k0 + b * kstep] = sqrtf(q / npix);
+                out[img * 2 * K + k0 + b] = m;
+                out[img * 2 * K + K + k0 + b] = sqrtf(q / npix);
             }
         }
     }
@@ -1248,59 +1244,6 @@ __device__ __forceinline__ void fold2_s2(const float2* __restrict__ H, int hld, 
                 d[0] = a0;
                 if (2 * pr[r] + 1 < npath) d[pslot] = a1;
             }
-        }
-    }
-}
-
-// s = 2 fold of a mirror batch: paths la and lb = L - 2 - la, whose filters satisfy
-// psi_lb(k1, k2) = psi_la(k1, -k2) (kymatio's theta grid is symmetric about 0; checked on the host per
-// level).  The lane of column v loads psi_la's four taps once (single-path floats) and folds path la
-// at (u, v) and path lb at (u, (n2 - v) mod n2), which uses the same four values with the columns
-// swapped: half the filter bytes per path of the pair layout, for four more spectrum reads from LDS.
-// fb != nullptr: a plain batch of two single-path filters instead (the paths without a mirror).
-// Slot 0 holds la, slot 1 lb.
-__device__ __forceinline__ void fold2_s2_mirror(const float2* __restrict__ H, int hld, int nM1, int nN1,
-                                                const float* __restrict__ fa, const float* __restrict__ fb,
-                                                float2* __restrict__ B, int pslot, int ld2, int nM2, int nN2) {
-    const int rpp = blockDim.x / nN2;
-    const int t0 = threadIdx.x / nN2;
-    if (t0 >= rpp) return;
-    const int v = threadIdx.x - t0 * nN2;
-    const bool v0 = v == 0;
-    const int cB = v0 ? nN2 : nN2 - v;   // column of la's conjugate taps = lb's output column (v > 0)
-    const float sg = v0 ? 1.f : -1.f;
-    const int w = v0 ? 0 : nN2 - v;
-    const int hq = nM2 * hld;
-    const int fq = nM2 * nN1;
-    for (int u = t0; u < nM2; u += rpp) {
-        const int hr = u * hld;
-        const int hm0 = v0 ? hr : (u == 0 ? 0 : (nM1 - u) * hld);   // row krm(u)
-        const int hm1 = v0 ? hr + hq : (nM2 - u) * hld;              // row krm(u + nM2)
-        float2 h0 = H[hr + v], h1 = H[hm0 + cB], h2 = H[hr + hq + v], h3 = H[hm1 + cB];
-        h1.y *= sg;
-        h3.y *= sg;
-        const int fo = u * nN1 + v;
-        const float f00 = fa[fo], f01 = fa[fo + nN2], f10 = fa[fo + fq], f11 = fa[fo + fq + nN2];
-        float2 a0, a1;
-        a0.x = fmaf(h0.x, f00, fmaf(h1.x, f01, fmaf(h2.x, f10, h3.x * f11)));
-        a0.y = fmaf(h0.y, f00, fmaf(h1.y, f01, fmaf(h2.y, f10, h3.y * f11)));
-        B[u * ld2 + v] = a0;
-        if (fb) {
-            const float g00 = fb[fo], g01 = fb[fo + nN2], g10 = fb[fo + fq], g11 = fb[fo + fq + nN2];
-            a1.x = fmaf(h0.x, g00, fmaf(h1.x, g01, fmaf(h2.x, g10, h3.x * g11)));
-            a1.y = fmaf(h0.y, g00, fmaf(h1.y, g01, fmaf(h2.y, g10, h3.y * g11)));
-            B[pslot + u * ld2 + v] = a1;
-        } else {
-            if (v0) {
-                a1 = a0;   // columns 0 and n2 are their own mirrors
-            } else {
-                // lb at (u, w): H~(u, w), H~(u, n1 - v) = conj H[krm(u)][v], and the same at u + n2;
-                // taps psi_la at columns n2 + v, v
-                const float2 e0 = H[hr + w], e1 = H[hm0 + v], e2 = H[hr + hq + w], e3 = H[hm1 + v];
-                a1.x = fmaf(e0.x, f01, fmaf(e1.x, f00, fmaf(e2.x, f11, e3.x * f10)));
-                a1.y = fmaf(e0.y, f01, fmaf(-e1.y, f00, fmaf(e2.y, f11, -e3.y * f10)));
-            }
-            B[pslot + u * ld2 + w] = a1;
         }
     }
 }
@@ -1741,15 +1684,6 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
         const int s2 = 1 << (j2 - j1);
         int pb = lay.bcap / pslot;                 // paths per batch (multiple of 2)
         pb = PB ? PB : max(2, min(pb & ~1, 2 * nq));
-        // L = 8 pair batches of an LDS-resident spectrum at s = 2: mirror batches (0, 6), (1, 5),
-        // (2, 4) and the plain batch (3, 7), when the host found the level's filters mirror-symmetric
-#ifndef WST_NO_MIRROR
-        constexpr bool MIRA = LC == 8 && PB == 2 && !HG;
-#else
-        constexpr bool MIRA = false;
-#endif
-        const long long* mo = p.psi2s_off + (j2 * J + j1) * L;
-        const bool mir = MIRA && s2 == 2 && mo[0] >= 0;
 #pragma unroll 1
         for (int l2a = 0; l2a < L; l2a += pb) {
             if (nsplit > 1) {
@@ -1758,24 +1692,12 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             }
             const int npath = (PB > 0 && LC % (PB > 0 ? PB : 1) == 0) ? PB : min(pb, L - l2a);
             const int npair = (npath + 1) >> 1;
-            int la = l2a, kstep = 1;
-            if (mir) {
-                const int bm = l2a >> 1;
-                la = bm < 3 ? bm : 3;
-                kstep = (bm < 3 ? 6 - bm : 7) - la;
-            }
-            if (mir) {
-                if (!(dbg & 8) && !(dbg & 256))
-                    fold2_s2_mirror(H, hld, nM1, nN1, p.psi2s + mo[la], la < 3 ? nullptr : p.psi2s + mo[la + kstep],
-                                    B, pslot, ld2, nM2, nN2);
-            } else {
-                const float2* ps = p.psi2 + p.psi2_off[(j2 * J + j1) * nq + (l2a >> 1)];
-                const long long pstride = static_cast<long long>(n1);
-                const int* bx = p.box + p.box_off[j2 * J + j1] + (l2a >> 1) * (nM2 + nN2);
-                if (!(dbg & 8) && !(dbg & (s2 == 2 ? 256 : 512)))
-                    fold2_any<WST_HG_R>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
-                              bx, nM2 + nN2);
-            }
+            const float2* ps = p.psi2 + p.psi2_off[(j2 * J + j1) * nq + (l2a >> 1)];
+            const long long pstride = static_cast<long long>(n1);
+            const int* bx = p.box + p.box_off[j2 * J + j1] + (l2a >> 1) * (nM2 + nN2);
+            if (!(dbg & 8) && !(dbg & (s2 == 2 ? 256 : 512)))
+                fold2_any<WST_HG_R>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
+                          bx, nM2 + nN2);
             __syncthreads();
             WST_STAMP(sctr);
             const float scale2 = 1.f / static_cast<float>(n1);
@@ -1785,14 +1707,14 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                     lds_fft_lines<FN, 0, PHI, kDR, true>(
                         B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, nN2, tb.twN(j2), id);
                 WST_STAMP(sctr);
-                const int k0 = kbase + (j2 - j1 - 1) * L + la;
+                const int k0 = kbase + (j2 - j1 - 1) * L + l2a;
                 float* outd = pooled ? nullptr : out + (img * p.K + k0) * (oM * oN);
                 if (!(dbg & 64))
                     family_cols_modlp<FM, 0, PHI>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
                                                        tb.gM(j2), tb.gN(j2), oms, oM, oN,
-                                                       scale2, S, outd, kstep);
+                                                       scale2, S, outd);
                 WST_STAMP(sctr);
-                if (!outd) emit(S, npath, k0, img, p.K, oM, oN, out, pooled, -1, 1, kstep);
+                if (!outd) emit(S, npath, k0, img, p.K, oM, oN, out, pooled);
             } else {
                 EpiModulus mod2{scale2, 0.f};
                 if (!(dbg & 16))

@@ -151,8 +151,6 @@ struct wst_plan {
     int* d_perm_off = nullptr;
     float2* d_psi2 = nullptr;
     long long* d_psi2_off = nullptr;
-    float* d_psi2s = nullptr;                     // single-path order-2 filters (mirror folds)
-    long long* d_psi2s_off = nullptr;
     int* d_box = nullptr;
     int* d_box_off = nullptr;
     int* d_box1_off = nullptr;
@@ -230,8 +228,6 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_perm_off);
     (void)hipFree(p->d_psi2);
     (void)hipFree(p->d_psi2_off);
-    (void)hipFree(p->d_psi2s);
-    (void)hipFree(p->d_psi2s_off);
     (void)hipFree(p->d_box);
     (void)hipFree(p->d_box_off);
     (void)hipFree(p->d_box1_off);
@@ -500,39 +496,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                     }
                 }
     }
-    // single-path filters of the s = 2 order-2 levels whose theta grid is mirror-symmetric:
-    // psi_{L-2-l}(k1, k2) == psi_l(k1, -k2) to 1e-12 of the filter maximum (kymatio's level-0
-    // filters; the periodised crops of levels r >= 1 treat the Nyquist bin asymmetrically and fail
-    // the check).  k_o2's mirror fold (fold2_s2_mirror) reads them; -1 = pair layout only.
-    std::vector<float> psi2s;
-    std::vector<long long> psi2s_off(static_cast<size_t>(J) * J * L, -1);
-    if (max_order >= 2 && L % 2 == 0 && L >= 4) {
-        for (int j2 = 1; j2 < J; ++j2) {
-            const int r = j2 - 1;
-            if (r >= wst::psi_levels(j2, J)) continue;
-            const int nM = g.PM >> r, nN = g.PN >> r;
-            bool ok = true;
-            for (int la = 0; la < (L - 2) / 2 && ok; ++la) {
-                const auto& fa = fb.psi[static_cast<size_t>(j2) * L + la][r];
-                const auto& fm = fb.psi[static_cast<size_t>(j2) * L + (L - 2 - la)][r];
-                double mx = 0.0;
-                for (double v : fm) mx = std::max(mx, std::fabs(v));
-                for (int kr = 0; kr < nM && ok; ++kr)
-                    for (int kc = 0; kc < nN; ++kc)
-                        if (std::fabs(fa[static_cast<size_t>(kr) * nN + (nN - kc) % nN] -
-                                      fm[static_cast<size_t>(kr) * nN + kc]) > 1e-12 * mx) {
-                            ok = false;
-                            break;
-                        }
-            }
-            if (!ok) continue;
-            for (int l = 0; l < L; ++l) {
-                psi2s_off[(static_cast<size_t>(j2) * J + r) * L + l] = static_cast<long long>(psi2s.size());
-                for (double v : fb.psi[static_cast<size_t>(j2) * L + l][r]) psi2s.push_back(static_cast<float>(v));
-            }
-        }
-    }
-    if (psi2s.empty()) psi2s.push_back(0.f);
     // alias boxes of the order-2 pairs (see fold2): per (j2, r) all pairs, stride nM2 + nN2
     std::vector<int> box;
     std::vector<int> box_off(static_cast<size_t>(J) * J, 0);
@@ -714,8 +677,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     if ((rc = upload(&plan->d_o2, o2)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_psi2, psi2)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_psi2_off, psi2_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_psi2s, psi2s)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_psi2s_off, psi2s_off)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_perm, perm)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_perm_off, t.perm_off)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_box, box)) != WST_OK) return rc;
@@ -745,7 +706,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     dp.perm = plan->d_perm; dp.perm_off = plan->d_perm_off;
     dp.o2_base = plan->d_o2;
     dp.psi2 = plan->d_psi2; dp.psi2_off = plan->d_psi2_off;
-    dp.psi2s = plan->d_psi2s; dp.psi2s_off = plan->d_psi2s_off;
     dp.box = plan->d_box; dp.box_off = plan->d_box_off; dp.box1_off = plan->d_box1_off;
     // the order-1 box-sparse fold pays off from s = 8 on (measured on MI355X at c2); order 2
     // uses it for every s >= 4
