@@ -153,3 +153,21 @@ def test_real_data_magnitude_sanity():
     assert 0.3 < S[:, 0].mean() < 0.7
     assert 1e-4 < S[:, 1:17].mean() < 0.2
     assert 1e-6 < S[:, 17:].mean() < S[:, 1:17].mean()
+
+
+@pytest.mark.parametrize("M,J,L", [(64, 4, 8), (128, 2, 8), (32, 3, 6)])
+def test_grid_symmetries_permute_orientations(M, J, L):
+    """SURVEY §4.4 rotation pin: rot90 permutes the orientation indices by L/2 (mod L), a row flip
+    by l -> L-2-l, a transpose by l -> L/2-2-l; S2 permutes in theta1 and theta2 (tests/symmetry.py)."""
+    from symmetry import exact_mask, grid_ops, symmetry_errors
+    s = kr.Scattering2D(J=J, shape=(M, M), L=L, pre_pad=True)
+    P = s.M_padded
+    x = np.random.default_rng(7).random((2, P, P))
+    Sx = s(x)
+    exact = exact_mask(J, L)
+    for name, (op, f, mapop) in grid_ops(P, J, L).items():
+        err = symmetry_errors(Sx, s(op(x)), J, L, f, mapop)
+        assert err[exact].max() < 1e-12, (name, err[exact].max())
+        if (~exact).any():
+            # level-j1 >= 1 crops of the masked periodisation keep only the negative Nyquist bin
+            assert 1e-6 < err[~exact].max() < 3e-3, (name, err[~exact].max())
