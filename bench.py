@@ -20,9 +20,11 @@ Extra JSON fields:
   roofline     : dominant kernel (largest HIP-event time of the step; k_o2 at j1=0 on c2)
                  algorithmic FLOP per launch / HIP-event launch time
                  vs the fp32 VALU peak (SURVEY §8(d) flop convention 5 n^2 log2 n^2 per n x n FFT);
-                 also vs FP32_meas (an FMA probe kernel timed in the same run);
                  traffic from committed rocprofv3 PMC passes when they match this library build.
-  measured     : BW_meas (streaming-copy probe) and FP32_meas (FMA probe), this run, this GPU.
+  measured     : BW_meas (streaming-copy probe) and FP32_meas (FMA probe), this run, this GPU
+                 (informational: the roofline is priced against the spec peaks only).
+  lib_built_from_src : the loaded libwst_hip.so is the one __graft_entry__.build() produced from
+                 these sources (libwst_hip.build.json; build_record says whether make recompiled).
   cpu_baseline : the float64 oracle (oracle/kymatio_ref.py, a port of kymatio 0.3.0) on the
                  host cores, rank 0 at every N, before the GPU is touched, bounded sample:
                  (i) run the way the reference runs it (plan rebuilt per patch, 3 serial channel
@@ -169,6 +171,20 @@ def src_sha():
         with open(p, "rb") as f:
             h.update(f.read())
     return h.hexdigest()[:16]
+
+
+def build_provenance():
+    """The record __graft_entry__.build() left beside the library: was the loaded .so built from
+    these sources (same src_sha) and is it the file that build produced (same lib_sha)?"""
+    from wst_amd import _lib
+    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libwst_hip.build.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return {"lib_built_from_src": None, "build_record": None}
+    return {"lib_built_from_src": rec.get("src_sha") == src_sha() and rec.get("lib_sha") == lib_sha(),
+            "build_record": {k: rec.get(k) for k in ("src_sha", "lib_sha", "rebuilt", "make_q_before")}}
 
 
 def pmc_file_config(name):
@@ -393,7 +409,7 @@ def measure_probes(torch, lib, dev, stream):
     measured, 97 % of the guide's 6.29; 2 GiB 5.93) and
     FP32_meas (32 independent FMA chains per lane, 16 waves per SIMD, long enough that launch and
     clock ramp do not count: 151 TF at 4096 x 256 threads x 16384 steps against 122-145 for shorter
-    runs, tools/probe_ab.py)."""
+    runs)."""
     from wst_amd import _lib
     nbytes = 1 << 30
     src = torch.ones(nbytes // 4, dtype=torch.float32, device=dev)
@@ -659,12 +675,15 @@ def main():
     sha = src_sha()
     dname = rocprof_name(dom, plan.PM, plan.PN, J)
     summary = pmc_summary(sha, args.config) or pmc_summary(lib_sha(), args.config)
-    rb = staged_levels(plan.PM, plan.PN, J)
+    rb, nst, _ = plan.staging()            # the plan's own level schedule (wst_plan_staging)
     if dom != "k_prep" and int(dom.split("=")[1]) >= rb:
         traffic = pmc_traffic(sha, dname, args.config) or pmc_traffic(lib_sha(), dname, args.config)
     else:   # composite slot of the staged levels: its kernels summed per chunk
-        nst = rb if (family(plan.PM) and plan.PM == plan.PN and plan.Mo <= 8) else J
         traffic = slot_traffic(summary, staged_sequence(plan.PM, plan.PN, J, L, nst), dom)
+        if traffic is None and summary is not None:
+            print(f"bench: warning: the PMC dispatch sequence of {summary.get('src_sha')} matches no "
+                  f"chunk of the staged launch order (rb={rb}, nst={nst}); roofline.traffic is null",
+                  file=sys.stderr, flush=True)
     avg_ms = kms[dom] / nchunks
     roofline = {
         "bound": "valu", "pipe": "fp32 VALU (LDS FFT butterflies; f32 MFMA only in the wide low-pass)",
@@ -681,9 +700,6 @@ def main():
         "all_kernels_tflops": round(planes * sum(flops.values()) / (sum(kms.values()) * 1e-3) / 1e12, 4),
         "src_sha": sha, "lib_sha": lib_sha(),
     }
-    if probes:
-        roofline["peak_measured"] = probes["fp32_tflops"]
-        roofline["frac_of_measured"] = round(achieved / probes["fp32_tflops"], 5)
     patch_flop = C * sum(flops.values())
     patch_bytes = C * M * N * 4 + (C * 2 * K * 4 if args.pooled else C * K * Mo * No * 4)
     rate_per_gpu = value / world
@@ -727,6 +743,7 @@ def main():
                                       f" of {'the coefficient tensor' if args.c3_output == 'full' else 'pooled features'}"},
             "roofline": roofline, "step_roofline": step_roof, "measured": probes, "cpu_baseline": cpu,
         }
+        line.update(build_provenance())
         if gather:
             line["gather"] = gather
         line.update(extra)

@@ -92,16 +92,23 @@ int wst_padded_shape(const wst_plan* plan, int* PM, int* PN);
  * Any smaller (non-zero) workspace is accepted: the batch is then processed in chunks. */
 int wst_workspace_bytes(const wst_plan* plan, int64_t nbatch, size_t* bytes);
 
+/* Internal workspaces (wst_forward with d_workspace == NULL) the plan holds: one per stream,
+ * at most 4 streams (a new stream evicts a buffer whose last work has completed, else the least
+ * recently used one once its work completes).  Lets callers and tests bound the plan's device
+ * memory. */
+int wst_internal_workspaces(const wst_plan* plan, int* count, size_t* bytes);
+
 /* Planes per workspace chunk the plan is tuned for (2048 for LDS-resident geometries; fewer for
  * geometries with HBM-staged levels, whose workspace is tens of MB per plane).  wst_forward
  * never processes more planes than this per chunk; size the workspace for
  * min(nbatch, preferred) planes.  (No kymatio counterpart: sizing helper of the batched ABI.) */
-/* Internal workspaces (wst_forward with d_workspace == NULL) the plan holds: one per stream,
- * at most 4 streams (a new stream evicts the least recently used buffer once its last work has
- * completed).  Lets callers and tests bound the plan's device memory. */
-int wst_internal_workspaces(const wst_plan* plan, int* count, size_t* bytes);
-
 int wst_preferred_batch(const wst_plan* plan, int64_t* planes);
+
+/* How the plan runs its levels (no kymatio counterpart; profiling / launch-sequence helper):
+ * rb = leading levels run HBM-staged (wst_staged.h), nst = levels with staged order-2 passes
+ * (rb, or J when no order-2 level folds from the global spectrum), sq = the square fused
+ * LDS-resident kernels are used. */
+int wst_plan_staging(const wst_plan* plan, int* rb, int* nst, int* sq);
 
 /*
  * Scattering of `nbatch` float32 planes.

@@ -160,4 +160,14 @@ def test_staged_lines_beyond_lds_tiles_are_unsupported():
     with pytest.raises(_lib.WSTError) as e:
         _lib.Plan(2048, 2048, 2, 2)                # 2056^2 padded: 2056-point lines
     assert e.value.code == _lib.WST_ERR_UNSUPPORTED
-    assert "1204 points" in str(e.value)
+    # the limit printed is the largest line the row / column tiles (and taps) actually admit
+    assert "at most 1203 points" in str(e.value), str(e.value)
+
+
+def test_staged_final_map_beyond_lds_is_unsupported():
+    # 1000^2 J=2: 1008-point staged lines fit the tiles, but the 250 x 250 output maps (250 KB)
+    # exceed k_big_final's LDS map: rejected at plan creation, not at wst_forward
+    with pytest.raises(_lib.WSTError) as e:
+        _lib.Plan(1000, 1000, 2, 8)
+    assert e.value.code == _lib.WST_ERR_UNSUPPORTED
+    assert "250x250 output maps" in str(e.value), str(e.value)

@@ -23,7 +23,7 @@ EXPORTS = (
     "wst_abi_version", "wst_last_error", "wst_default_convention", "wst_plan_create",
     "wst_plan_create_ex", "wst_plan_destroy",
     "wst_output_shape", "wst_padded_shape", "wst_workspace_bytes", "wst_preferred_batch",
-    "wst_internal_workspaces",
+    "wst_internal_workspaces", "wst_plan_staging",
     "wst_forward",
     "wst_forward_profiled", "wst_host_filter", "wst_host_filter_ex", "wst_host_fft_lines",
     "wst_salt_pepper_counts", "wst_noise_apply", "wst_noise_generate", "wst_advanced_stats",
@@ -127,6 +127,8 @@ def load() -> ctypes.CDLL:
         lib.wst_aux_last_error.argtypes = []
         lib.wst_preferred_batch.restype = c_int
         lib.wst_preferred_batch.argtypes = [c_vp, ctypes.POINTER(c_i64)]
+        lib.wst_plan_staging.restype = c_int
+        lib.wst_plan_staging.argtypes = [c_vp] + [ctypes.POINTER(c_int)] * 3
         lib.wst_internal_workspaces.restype = c_int
         lib.wst_internal_workspaces.argtypes = [c_vp, ctypes.POINTER(c_int), ctypes.POINTER(c_sz)]
         lib.wst_forward.restype = c_int
@@ -221,6 +223,12 @@ class Plan:
         b = ctypes.c_int64()
         check(load().wst_preferred_batch(self._h, ctypes.byref(b)))
         return b.value
+
+    def staging(self):
+        """(rb, nst, sq) of the plan's level schedule (wst_plan_staging)."""
+        rb, nst, sq = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(load().wst_plan_staging(self._h, ctypes.byref(rb), ctypes.byref(nst), ctypes.byref(sq)))
+        return rb.value, nst.value, sq.value
 
     def internal_workspaces(self):
         """(count, bytes) of the per-stream internal workspaces (wst_internal_workspaces)."""

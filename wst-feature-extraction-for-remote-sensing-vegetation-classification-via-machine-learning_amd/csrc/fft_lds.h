@@ -206,16 +206,6 @@ WST_HD void rfft(float2 (&x)[R]) {
 // four-step line transforms
 // ---------------------------------------------------------------------------------------------
 constexpr int split_n2(int n) {  // N2 = largest divisor <= sqrt(n); 1 means a single stage
-    // per-size overrides (A/B build knobs; host tables and kernels must agree: build both)
-#ifdef WST_SPLIT24
-    if (n == 24) return WST_SPLIT24;
-#endif
-#ifdef WST_SPLIT48
-    if (n == 48) return WST_SPLIT48;
-#endif
-#ifdef WST_SPLIT96
-    if (n == 96) return WST_SPLIT96;
-#endif
     if (n <= 16 || is_prime(n)) return 1;
     int best = 1;
     for (int d = 2; d * d <= n; ++d)

@@ -28,24 +28,6 @@
 
 #include "fft_lds.h"
 
-// WST_STAMPS (diagnostic builds only): thread 0 of the first kStampBlocks workgroups of k_o2
-// records s_memtime at its phase boundaries into wst_stamps (read back by wst_dbg_stamps_*).
-#ifdef WST_STAMPS
-constexpr int kStampBlocks = 512, kStampSlots = 64;
-__device__ unsigned long long wst_stamps[kStampBlocks * kStampSlots];
-#define WST_STAMP(ctr)                                                                     \
-    do {                                                                                   \
-        if (stamp_on && threadIdx.x == 0 && blockIdx.x < kStampBlocks && (ctr) < kStampSlots)          \
-            wst_stamps[blockIdx.x * kStampSlots + (ctr)] = __builtin_amdgcn_s_memtime();   \
-        ++(ctr);                                                                           \
-    } while (0)
-#else
-#define WST_STAMP(ctr) do {} while (0)
-#endif
-#ifndef WST_LP_TILED
-#define WST_LP_TILED 1  // register-tiled separable low-pass for outputs wider than 8 (lds_lowpass)
-#endif
-
 // Phase-skipping ablation mask (DevParams::dbg_skip): compiled in only for diagnostic builds
 // (-DWST_DIAG); production kernels see a constant 0 and carry no skip branches.
 #ifdef WST_DIAG
@@ -440,7 +422,7 @@ __device__ __forceinline__ void lds_lowpass(float2* U, int nb, int bs, int rows,
                                             const int* permN, int s, int oM, int oN, float* S) {
     if (oN <= 4)
         lds_lowpass_t<4, 8, 16>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, S);
-    else if (oN <= 8 || !WST_LP_TILED)
+    else if (oN <= 8)
         lds_lowpass_t<8, 8, 16>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s, oM, oN, S);
     else
         lds_lowpass_tiled<4, 8, 8, 4, 4, 8>(U, nb, bs, rows, cols, ld, hM2, hN2, permM, permN, s,
@@ -450,9 +432,6 @@ __device__ __forceinline__ void lds_lowpass(float2* U, int nb, int bs, int rows,
 // Block-size bound of the exported-spectrum k_o2 (HG, non-SQ: f3 / c1 geometries).  A 512 bound
 // lets the compiler use 160 VGPRs instead of the 128 of a 1024 bound (f3: 11 VGPRs spilled), but
 // measured: f3 k_o2 1.53 -> 1.94-2.83 ms (256-512 threads), c1 1.50 -> 1.46; kept at 1024.
-#ifndef WST_O2X_BOUND
-#define WST_O2X_BOUND 1024
-#endif
 constexpr int kLpOM = 8;  // row stride of the GM tap matrices = largest oM of the fused path
 
 // Separable phi low-pass on the matrix cores (v_mfma_f32_16x16x4_f32: exact fp32, the fmaf chain
@@ -951,24 +930,13 @@ __host__ __device__ inline int odd_ld(int n) { return n | 1; }
 // Streaming (non-temporal) 8-byte load / store: the half-spectrum hand-off k_o1 -> k_o2 is
 // written and read once (~0.9 GB per 2048-plane chunk at the 96^2 level), kept from displacing
 // the filters the folds re-read from L2 (c2: -2.5 %, measured).
-#ifndef WST_NT_HANDOFF
-#define WST_NT_HANDOFF 1   // 0: default-policy hand-off loads / stores (A/B builds)
-#endif
 __device__ __forceinline__ float2 ldnt(const float2* p) {
-#if WST_NT_HANDOFF
     return __builtin_bit_cast(float2,
                               __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(p)));
-#else
-    return *p;
-#endif
 }
 __device__ __forceinline__ void stnt(float2* p, float2 v) {
-#if WST_NT_HANDOFF
     __builtin_nontemporal_store(v.x, &p->x);
     __builtin_nontemporal_store(v.y, &p->y);
-#else
-    *p = v;
-#endif
 }
 
 // dst[i] = src[i] for i < n (global -> LDS): eight loads per thread in flight before the stores
@@ -986,11 +954,7 @@ __device__ __forceinline__ void copy_to_lds(float2* dst, const float2* __restric
             f4v t[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-#if WST_NT_HANDOFF
                 t[k] = __builtin_nontemporal_load(s4 + min(i0 + k * T, n4 - 1));
-#else
-                t[k] = s4[min(i0 + k * T, n4 - 1)];
-#endif
             }
 #pragma unroll
             for (int k = 0; k < K; ++k)
@@ -1248,77 +1212,11 @@ __device__ __forceinline__ void fold2_s2(const float2* __restrict__ H, int hld, 
     }
 }
 
-// s = 2 fold, PU pairs of the batch from one read of the four spectrum taps: the lane of column
-// v walks the (pair group, row u) items, reads H's taps once per item and folds its PU pairs
-// (PU x 4 filter loads in flight), so the batch reads the spectrum npair / PU times, not npair.
-template <int PU = 2>
-__device__ __forceinline__ void fold2_s2_pairs(const float2* __restrict__ H, int hld, int nM1, int nN1,
-                                               const float2* __restrict__ psi2, long long pstride,
-                                               int npair, int npath, float2* __restrict__ B, int pslot,
-                                               int ld2, int nM2, int nN2) {
-    const int rpp = blockDim.x / nN2;
-    const int t0 = threadIdx.x / nN2;
-    if (t0 >= rpp) return;
-    const int v = threadIdx.x - t0 * nN2;
-    const bool v0 = v == 0;
-    const int cB = v0 ? nN2 : nN2 - v;
-    const float sg = v0 ? 1.f : -1.f;
-    const int hq = nM2 * hld;
-    const int fq = nM2 * nN1 * 8;
-    const int ps8 = static_cast<int>(pstride * 8);
-    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, static_cast<int>(npair * pstride * 8));
-    const int ngrp = (npair + PU - 1) / PU;
-    const wstfft::FastDiv dm(nM2);
-    for (int gu = t0; gu < ngrp * nM2; gu += rpp) {
-        const int g = dm.div(gu);
-        const int u = gu - g * nM2;
-        const int pr0 = g * PU;
-        const int hr = u * hld;
-        const int hm0 = v0 ? hr : (u == 0 ? 0 : (nM1 - u) * hld);
-        const int hm1 = v0 ? hr + hq : (nM2 - u) * hld;
-        float2 h0 = H[hr + v], h1 = H[hm0 + cB], h2 = H[hr + hq + v], h3 = H[hm1 + cB];
-        h1.y *= sg;
-        h3.y *= sg;
-        const int fo = (u * nN1 + v) * 8;
-        float2* d0 = B + u * ld2 + v;
-        {
-            float2 f[PU][4];
-#pragma unroll
-            for (int r = 0; r < PU; ++r) {
-                const int so = min(pr0 + r, npair - 1) * ps8;
-                f[r][0] = buf_load2(rs, fo, so);
-                f[r][1] = buf_load2(rs, fo, so + nN2 * 8);
-                f[r][2] = buf_load2(rs, fo, so + fq);
-                f[r][3] = buf_load2(rs, fo, so + fq + nN2 * 8);
-            }
-#pragma unroll
-            for (int r = 0; r < PU; ++r) {
-                const int pr = pr0 + r;
-                if (pr >= npair) break;
-                float2 a0, a1;
-                a0.x = fmaf(h0.x, f[r][0].x, fmaf(h1.x, f[r][1].x, fmaf(h2.x, f[r][2].x, h3.x * f[r][3].x)));
-                a0.y = fmaf(h0.y, f[r][0].x, fmaf(h1.y, f[r][1].x, fmaf(h2.y, f[r][2].x, h3.y * f[r][3].x)));
-                a1.x = fmaf(h0.x, f[r][0].y, fmaf(h1.x, f[r][1].y, fmaf(h2.x, f[r][2].y, h3.x * f[r][3].y)));
-                a1.y = fmaf(h0.y, f[r][0].y, fmaf(h1.y, f[r][1].y, fmaf(h2.y, f[r][2].y, h3.y * f[r][3].y)));
-                float2* d = d0 + 2 * pr * pslot;
-                d[0] = a0;
-                if (2 * pr + 1 < npath) d[pslot] = a1;
-            }
-        }
-    }
-}
-
 template <int R = 1>
 __device__ __forceinline__ void fold2_any(int s2, const float2* H, int hld, int nM1, int nN1,
                                           const float2* psi2, long long pstride, int npair,
                                           int npath, float2* B, int pslot, int ld2, int nM2,
                                           int nN2, const int* box, int bstride) {
-#ifdef WST_FOLD_PAIRS
-    if (s2 == 2 && R == 1) {
-        fold2_s2_pairs<WST_FOLD_PAIRS>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
-        return;
-    }
-#endif
     if (s2 == 2) fold2_s2<R>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
     else fold2<0>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, s2, box, bstride);
 }
@@ -1566,7 +1464,6 @@ __global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevPara
             return;
         }
     }
-#ifndef WST_NO_N1T
     if constexpr (!SQ && FM == FN && FM > 0) {
         // square levels of the family's sizes in this class: compile-time level size (f3 / c1)
         if (p.PM == p.PN) {
@@ -1583,7 +1480,6 @@ __global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevPara
             if (done) return;
         }
     }
-#endif
     k_o1_body<FM, FN, MAXN, SQ, 0>(smem, p, lay, j1, nimg, img0, xhat, hexp, out, pooled);
 }
 
@@ -1603,9 +1499,6 @@ constexpr int o2_min_waves(int cap) { return cap == 48 ? 6 : cap == 24 ? 5 : 1; 
 // deeper level in one batch of all LC paths (the layout's B holds LC paths of level j1 + 2, so of
 // every level below it), so each batch shape -- paths, pairs, lines, loop bounds and divisors --
 // folds at compile time.
-#ifndef WST_HG_R
-#define WST_HG_R (HG ? 2 : 1)
-#endif
 template <int FM, int FN, int MAXN, int SQ, int HG, int OC, int LC = 0>
 __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& p,
                                           const LdsLayout& lay, int j1, int nimg, long long img0,
@@ -1654,9 +1547,6 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     const Tables tb = load_tables(p, lay, smem);
     const int dbg = WST_DBG_MASK(p);
     wstfft::EpiIdentity id;
-    [[maybe_unused]] int sctr = 0;
-    [[maybe_unused]] const bool stamp_on = (j1 == 0);
-    WST_STAMP(sctr);
     // order-2 path sizes: <= MAXN / 2 below an LDS-resident level of class MAXN, <= MAXN after a
     // big level
     constexpr int PHI = (SQ && !HG) ? MAXN / 2 : MAXN;
@@ -1670,7 +1560,6 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(
                 Hl, wstfft::Lines{1, 0, hld, 1, hld}, nM1, tb.twM(j1), id);
     }
-    WST_STAMP(sctr);
 
     // 2. order-2 paths in batches: Hermitian fold -> |ifft| -> S2 low-pass
     const int kbase = p.o2_base[j1 * L + l1];
@@ -1696,24 +1585,21 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             const long long pstride = static_cast<long long>(n1);
             const int* bx = p.box + p.box_off[j2 * J + j1] + (l2a >> 1) * (nM2 + nN2);
             if (!(dbg & 8) && !(dbg & (s2 == 2 ? 256 : 512)))
-                fold2_any<WST_HG_R>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
+                fold2_any<HG ? 2 : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
                           bx, nM2 + nN2);
             __syncthreads();
-            WST_STAMP(sctr);
             const float scale2 = 1.f / static_cast<float>(n1);
             if constexpr (SQ) {
                 // rows, then the column pass fused with |.| and the S2 low-pass
                 if (!(dbg & 16))
                     lds_fft_lines<FN, 0, PHI, kDR, true>(
                         B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, nN2, tb.twN(j2), id);
-                WST_STAMP(sctr);
                 const int k0 = kbase + (j2 - j1 - 1) * L + l2a;
                 float* outd = pooled ? nullptr : out + (img * p.K + k0) * (oM * oN);
                 if (!(dbg & 64))
                     family_cols_modlp<FM, 0, PHI>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
                                                        tb.gM(j2), tb.gN(j2), oms, oM, oN,
                                                        scale2, S, outd);
-                WST_STAMP(sctr);
                 if (!outd) emit(S, npath, k0, img, p.K, oM, oN, out, pooled);
             } else {
                 EpiModulus mod2{scale2, 0.f};
@@ -1796,32 +1682,28 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
 
 
 template <int FM, int FN, int MAXN, int SQ, int HG = 0>
-__global__ void __launch_bounds__((HG && !SQ) ? WST_O2X_BOUND : 1024, o2_min_waves(MAXN)) k_o2(DevParams p, LdsLayout lay, int j1, int nimg,
+__global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, LdsLayout lay, int j1, int nimg,
                                              long long img0, const float2* __restrict__ hexp,
                                              float* __restrict__ out, int pooled, int j2first) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if constexpr (SQ) {
         if (p.oM == 4 && p.oN == 4 && lay.oms == 4) {
-#ifndef WST_NO_LC8
             if constexpr (!HG && unique_level(FM, MAXN) > 0) {
                 if (p.L == 8) {
                     k_o2_body<FM, FN, MAXN, SQ, HG, 4, 8>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
                     return;
                 }
             }
-#endif
             k_o2_body<FM, FN, MAXN, SQ, HG, 4>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
             return;
         }
     }
-#ifndef WST_NO_LC8
     if constexpr (!SQ && HG && FM == FN && FM > 0) {
         if (p.L == 8) {
             k_o2_body<FM, FN, MAXN, SQ, HG, 0, 8>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
             return;
         }
     }
-#endif
     k_o2_body<FM, FN, MAXN, SQ, HG, 0>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
 }
 

@@ -406,16 +406,38 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     wst::Geometry g;
     std::string err;
     if (!wst::make_geometry(M, N, J, L, max_order, g, err)) return fail(WST_ERR_INVALID, err);
-    // staged levels hold 2 kBigRows row lines / kColTile column lines of their level in LDS:
-    // checked before the (size-proportional) filter bank is built
-    for (int r = 0; r < J && std::max(g.PM, g.PN) >> r > wstbig::kBigMinN; ++r) {
-        const size_t nl = static_cast<size_t>(std::max(g.PM, g.PN) >> r);
-        const size_t lines = std::max<size_t>(2 * kBigRows, wstbig::kColTile);
-        if ((nl + lines * (nl | 1)) * sizeof(float2) > static_cast<size_t>(kMaxLds))
+    // staged levels hold 2 kBigRows row lines / kColTile column lines of their level in LDS (the
+    // column pass also its tap matrix when the maps are at most kLpOM wide): checked before the
+    // (size-proportional) filter bank is built, with the same formula as the plan's big_*_lds
+    {
+        const int omax = std::max(g.oM, g.oN);
+        const size_t tapw = omax <= wstdev::kLpOM ? static_cast<size_t>(std::max(omax <= 4 ? 4 : wstdev::kLpOM,
+                                                                                  (omax + 3) & ~3))
+                                                  : 0;
+        const auto fits = [&](size_t nl) {
+            const size_t lines = std::max<size_t>(2 * kBigRows, wstbig::kColTile);
+            return (nl + lines * (nl | 1)) * sizeof(float2) + nl * tapw * sizeof(float) <=
+                   static_cast<size_t>(kMaxLds);
+        };
+        for (int r = 0; r < J && std::max(g.PM, g.PN) >> r > wstbig::kBigMinN; ++r) {
+            const size_t nl = static_cast<size_t>(std::max(g.PM, g.PN) >> r);
+            if (!fits(nl)) {
+                size_t lim = nl;
+                while (lim > 0 && !fits(lim)) --lim;
+                return fail(WST_ERR_UNSUPPORTED, "padded plane " + std::to_string(g.PM) + "x" +
+                                                     std::to_string(g.PN) + ": staged level " + std::to_string(r) +
+                                                     " lines of " + std::to_string(nl) +
+                                                     " points exceed the LDS line tiles (160 KiB per CU; at most " +
+                                                     std::to_string(lim) + " points)");
+            }
+        }
+        // k_big_final holds one whole oM x oN output map in dynamic LDS
+        if (std::max(g.PM, g.PN) > wstbig::kBigMinN &&
+            static_cast<size_t>(g.oM) * g.oN * sizeof(float) > static_cast<size_t>(kMaxLds - 256))
             return fail(WST_ERR_UNSUPPORTED, "padded plane " + std::to_string(g.PM) + "x" + std::to_string(g.PN) +
-                                                 ": staged level " + std::to_string(r) + " lines of " +
-                                                 std::to_string(nl) + " points exceed the LDS line tiles " +
-                                                 "(160 KiB per CU; at most 1204 points)");
+                                                 ": its " + std::to_string(g.oM) + "x" + std::to_string(g.oN) +
+                                                 " output maps exceed the staged final pass's LDS map (at most " +
+                                                 std::to_string((kMaxLds - 256) / 4) + " values)");
     }
     wst::FilterBank fb;
     try {
@@ -956,7 +978,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         plan->o2_export[j1] = 1;
         plan->o2x_lds[j1] = lds;
         plan->o2x_threads[j1] = std::min(fill_cu(default_threads(static_cast<size_t>(nM1) * nN1), lds, 768),
-                                         WST_O2X_BOUND);
+                                         1024);
         plan->o1_lay[j1].export_full = 1;
         // one workgroup per item: splitting its batches over 2 / 4 workgroups of one XCD (as the
         // HG launches after staged levels do) measured slower here (f3 k_o2 1.57 -> 1.67 / 1.66 ms,
@@ -1031,6 +1053,14 @@ int wst_internal_workspaces(const wst_plan* plan, int* count, size_t* bytes) {
     size_t b = 0;
     for (const auto& kv : plan->ws_by_stream) b += kv.second.bytes;
     *bytes = b;
+    return WST_OK;
+}
+
+int wst_plan_staging(const wst_plan* plan, int* rb, int* nst, int* sq) {
+    if (!plan || !rb || !nst || !sq) return fail(WST_ERR_INVALID, "plan/rb/nst/sq is NULL");
+    *rb = plan->rb;
+    *nst = plan->rb > 0 ? plan->nst : 0;
+    *sq = plan->sq;
     return WST_OK;
 }
 
@@ -1290,13 +1320,31 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
         ws_lock = std::unique_lock<std::mutex>(plan->ws_mu);
         if (plan->ws_by_stream.find(stream) == plan->ws_by_stream.end() &&
             plan->ws_by_stream.size() >= kMaxStreamWs) {
-            auto lru = plan->ws_by_stream.begin();
-            for (auto it = plan->ws_by_stream.begin(); it != plan->ws_by_stream.end(); ++it)
-                if (it->second.tick < lru->second.tick) lru = it;
-            if (lru->second.done) WST_HIP_CHECK(hipEventSynchronize(lru->second.done));
-            if (lru->second.ptr) (void)hipFree(lru->second.ptr);
-            if (lru->second.done) (void)hipEventDestroy(lru->second.done);
-            plan->ws_by_stream.erase(lru);
+            // prefer an entry whose last work has already completed (least recently used among
+            // those); otherwise take the LRU entry out of the map and wait for it with the lock
+            // dropped, so other streams' calls on this plan do not block behind it
+            auto lru = plan->ws_by_stream.end(), idle = plan->ws_by_stream.end();
+            for (auto it = plan->ws_by_stream.begin(); it != plan->ws_by_stream.end(); ++it) {
+                if (lru == plan->ws_by_stream.end() || it->second.tick < lru->second.tick) lru = it;
+                const bool done = !it->second.done || hipEventQuery(it->second.done) == hipSuccess;
+                if (done && (idle == plan->ws_by_stream.end() || it->second.tick < idle->second.tick)) idle = it;
+            }
+            const bool have_idle = idle != plan->ws_by_stream.end();
+            const auto victim = have_idle ? idle : lru;
+            const wst_plan::StreamWs ev = victim->second;
+            plan->ws_by_stream.erase(victim);
+            if (!have_idle && ev.done) {
+                ws_lock.unlock();
+                const hipError_t se = hipEventSynchronize(ev.done);
+                ws_lock.lock();
+                if (se != hipSuccess) {
+                    if (ev.ptr) (void)hipFree(ev.ptr);
+                    (void)hipEventDestroy(ev.done);
+                    WST_HIP_CHECK(se);
+                }
+            }
+            if (ev.ptr) (void)hipFree(ev.ptr);
+            if (ev.done) (void)hipEventDestroy(ev.done);
         }
         wst_plan::StreamWs& sw = plan->ws_by_stream[stream];
         sw.tick = ++plan->ws_tick;

@@ -113,20 +113,3 @@ const FamilyOps& WST_GETTER_EXPAND(WST_FAM_M, WST_FAM_N)() {
 }
 
 }  // namespace wstlaunch
-
-#ifdef WST_STAMPS
-// diagnostic read-back of this family's k_o2 phase stamps (WST_STAMPS builds only)
-#define WST_STAMP_FN(A, B) wst_dbg_stamps_##A##_##B
-#define WST_STAMP_FN2(A, B) WST_STAMP_FN(A, B)
-extern "C" int WST_STAMP_FN2(WST_FAM_M, WST_FAM_N)(unsigned long long* host, int n) {
-    const int cap = kStampBlocks * kStampSlots;
-    return static_cast<int>(hipMemcpyFromSymbol(host, HIP_SYMBOL(wst_stamps),
-                                                sizeof(unsigned long long) * (n < cap ? n : cap)));
-}
-#define WST_CLEAR_FN(A, B) wst_dbg_clear_##A##_##B
-#define WST_CLEAR_FN2(A, B) WST_CLEAR_FN(A, B)
-extern "C" int WST_CLEAR_FN2(WST_FAM_M, WST_FAM_N)(void) {
-    static unsigned long long z[kStampBlocks * kStampSlots];
-    return static_cast<int>(hipMemcpyToSymbol(HIP_SYMBOL(wst_stamps), z, sizeof(z)));
-}
-#endif

@@ -25,10 +25,7 @@ using wstdev::DevParams;
 
 constexpr int kBigMinN = wstfft::kMaxFamilyN;   // levels with n > kBigMinN are staged
 constexpr int kBigThreads = 256;
-#ifndef WST_COL_TILE
-#define WST_COL_TILE 16
-#endif
-constexpr int kColTile = WST_COL_TILE;          // columns per column-pass workgroup (128 B rows)
+constexpr int kColTile = 16;         // columns per column-pass workgroup (128 B rows)
 constexpr int kMeanParts = 16;                  // k_big_mean partial sums per plane
 constexpr int kLoadBatch = 8;                   // global loads per thread in flight (tile loads)
 constexpr int kBigOGroup = 16;                  // outputs per accumulation round of wide low-passes
