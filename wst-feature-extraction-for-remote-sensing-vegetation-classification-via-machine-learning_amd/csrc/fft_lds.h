@@ -479,6 +479,14 @@ __device__ __forceinline__ void fft_lines_dr(float2* base, const Lines g, const 
     }
     __syncthreads();
 }
+// Stage B alone of F_DR (stage A done by the caller, e.g. fused with a fold).  Ends with a barrier.
+template <int N, bool INV, class Epi>
+__device__ __forceinline__ void fft_lines_dr_stageB(float2* base, const Lines g, Epi& epi) {
+    using F = LineFFT<N, INV>;
+    static_assert(F::N2 > 1, "two-stage sizes only");
+    for (int u = threadIdx.x; u < g.nlines() * F::N1; u += blockDim.x) F::stageB_inplace(base, g, u, epi);
+    __syncthreads();
+}
 // In-place digit-reversed -> natural transform (G).  Ends with a barrier.
 template <int N, bool INV, class Epi>
 __device__ __forceinline__ void fft_lines_rd(float2* base, const Lines g, const float2* tw, Epi& epi) {

@@ -36,6 +36,16 @@
 #define WST_DBG_MASK(p) 0
 #endif
 
+#ifndef WST_FUSE_MIN
+#define WST_FUSE_MIN 48
+#endif
+#ifndef WST_FUSE1_MIN
+#define WST_FUSE1_MIN 48
+#endif
+#ifndef WST_FUSE_GRP
+#define WST_FUSE_GRP 4
+#endif
+
 namespace wstdev {
 
 constexpr int kMaxLds = 160 * 1024;
@@ -72,6 +82,13 @@ struct DevParams {
     const float* lpw;
     const int* lpw_off;
     int oMp, oNp;
+    // order-2 tile tap lists of square levels at s = 4 / 8 (fold2_tile_list): per (j2, r) the
+    // headers of pair 0's tiles at taph + taph_off[j2*J + r] (int4 {first tap, direct groups of 4,
+    // mirrored groups of 4, 0} per (pair, tile of 64 bins)); taps: (LDS byte offset, filter byte
+    // offset) pairs relative to a lane's bases
+    const int4* taph;
+    const int* taph_off;
+    const int2* taps;
 };
 
 // Per-launch LDS layout (byte offsets) and the table slices copied into LDS.
@@ -1015,6 +1032,42 @@ __device__ __forceinline__ void fold1(const float2* __restrict__ X, const float*
     }
 }
 
+// s = 1 order-1 "fold" (Xhat * psi0, level 0) fused with stage A of the inverse row transform
+// (F_DR, two-stage N = NA * NB): unit (u, n2) multiplies the elements v = n2 + NB e of row u
+// straight from HBM / L2 into registers, runs the DFT-NA and the twiddles and stores the stage-A
+// result (the product is never written to LDS and read back).  Stage B follows after a barrier.
+template <int N>
+__device__ __forceinline__ void fold1_rowA(const float2* __restrict__ X, const float* __restrict__ psi0,
+                                           float2* __restrict__ A, const float2* __restrict__ tw) {
+    using F = wstfft::LineFFT<N, true>;
+    static_assert(F::N2 > 1, "two-stage row sizes only");
+    constexpr int NA = F::N1, NB = F::N2, LD = N | 1;
+    int w0 = threadIdx.x;
+    asm volatile("" : "+v"(w0));   // no hoisting of the unit's bases / twiddles (see fold2_s2_rowA)
+    for (int w = w0; w < N * NB; w += blockDim.x) {
+        const int u = w / NB, n2 = w - u * NB;
+        const float2* xr = X + u * N + n2;
+        const float* pr = psi0 + u * N + n2;
+        float2 x[NA];
+        wstfft::static_for<0, NA>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            const float2 xv = xr[NB * e];
+            const float f = pr[NB * e];
+            x[e] = make_float2(xv.x * f, xv.y * f);
+        });
+        wstfft::rfft<NA, true>(x);
+        wstfft::static_for<1, NA>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            x[k] = wstfft::cmul_tw(x[k], tw[n2 * k], true);
+        });
+        float2* d = A + u * LD + n2;
+        wstfft::static_for<0, NA>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            d[NB * e] = x[e];
+        });
+    }
+}
+
 // Box-sparse order-1 fold (s >= 4): aliases i in [i0, i0 + ni) of row u and j in [j0, j0 + nj) of
 // column v only (see fold2 / box tables); predicated blocks of 4 keep the loads in flight.
 __device__ __forceinline__ void fold1_box(const float2* __restrict__ X, const float* __restrict__ psi0,
@@ -1221,6 +1274,194 @@ __device__ __forceinline__ void fold2_any(int s2, const float2* H, int hld, int 
     else fold2<0>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, s2, box, bstride);
 }
 
+// ---- tile-mapped folds of a square level with compile-time sizes (SQ geometry kernels) ----
+// The npair x N2^2 (pair, bin) outputs of a batch go to whole waves in tiles of 64 consecutive
+// bins of one pair (wave-uniform tile loop), so every alias of a tile is one uniform offset from
+// two per-lane bases: the direct tap (a, b) of bin (u, v) (b < s/2: column v + N2 b < N1/2) reads
+// H[u + N2 a][v + N2 b] = dbase + (N2 a HLD + N2 b), the mirrored one (b >= s/2) reads
+// conj(H[(N1 - u - N2 a) % N1][N1 - v - N2 b]) = mbase + (N2 (s-1-a) HLD + N2 (s-1-b)) with
+// mbase = (N2 - u) HLD + (N2 - v) (H carries row N1 = row 0 for u = a = 0), and the filter pair
+// sits at fbase + (N2 a N1 + N2 b) with fbase = u N1 + v.  The tap offsets are compile-time
+// immediates (s = 2, dense) or come from host-built per-tile tap lists (s = 4, 8: only the
+// aliases where some bin of the tile meets a significant bin of either filter).
+__device__ __forceinline__ float2 lds_at(const char* base, int byte_off) {
+    return *reinterpret_cast<const float2*>(base + byte_off);
+}
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+// read-only table in the constant address space: loads at wave-uniform addresses become s_load
+typedef const __attribute__((address_space(4))) int* cint_p;
+template <typename T>
+__device__ __forceinline__ cint_p to_const_as(const T* p) {
+    return (cint_p)(reinterpret_cast<unsigned long long>(p));
+}
+
+template <int N1>
+__device__ __forceinline__ void fold2_tile_s2(const float2* __restrict__ H, const float2* __restrict__ psi2,
+                                              int npair, int npath, float2* __restrict__ B) {
+    constexpr int N2 = N1 / 2, HLD = N1 / 2 + 1, LD2 = N2 | 1, PSLOT = N2 * LD2;
+    constexpr int ITEMS = N2 * N2, NT = (ITEMS + 63) / 64, PST = N1 * N1;
+    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, npair * PST * 8);
+    const char* Hb = reinterpret_cast<const char*>(H);
+    const int w0 = wave_id();
+    for (int k = 0;; ++k) {
+        // wave-uniform tile index (readfirstlane: scalar loop control, pair and header offsets)
+        const int wi = __builtin_amdgcn_readfirstlane(w0 + k * nw);
+        if (wi >= npair * NT) break;
+        const int pr = wi / NT;
+        const int bin0 = (wi - pr * NT) * 64 + lane;
+        const int bin = min(bin0, ITEMS - 1);
+        const int u = bin / N2, v = bin - u * N2;
+        const int db = (u * HLD + v) * 8, mb = ((N2 - u) * HLD + (N2 - v)) * 8;
+        const int fo = (u * N1 + v) * 8, po = pr * PST * 8;
+        const float2 h0 = lds_at(Hb, db), h1 = lds_at(Hb, db + N2 * HLD * 8);   // (0,0) (1,0)
+        const float2 m0 = lds_at(Hb, mb + N2 * HLD * 8), m1 = lds_at(Hb, mb);   // (0,1) (1,1)
+        const float2 f0 = buf_load2(rs, fo, po), f1 = buf_load2(rs, fo, po + N2 * N1 * 8);
+        const float2 g0 = buf_load2(rs, fo, po + N2 * 8), g1 = buf_load2(rs, fo, po + (N2 * N1 + N2) * 8);
+        float2 a0, a1;
+        a0.x = fmaf(h0.x, f0.x, fmaf(h1.x, f1.x, fmaf(m0.x, g0.x, m1.x * g1.x)));
+        a0.y = fmaf(h0.y, f0.x, fmaf(h1.y, f1.x, fmaf(-m0.y, g0.x, -m1.y * g1.x)));
+        a1.x = fmaf(h0.x, f0.y, fmaf(h1.x, f1.y, fmaf(m0.x, g0.y, m1.x * g1.y)));
+        a1.y = fmaf(h0.y, f0.y, fmaf(h1.y, f1.y, fmaf(-m0.y, g0.y, -m1.y * g1.y)));
+        if (bin0 < ITEMS) {
+            float2* d = B + 2 * pr * PSLOT + u * LD2 + v;
+            d[0] = a0;
+            if (2 * pr + 1 < npath) d[PSLOT] = a1;
+        }
+    }
+}
+
+// s = 2 fold fused with stage A of the inverse row transform (F_DR order, two-stage sizes
+// N2 = NA * NB): unit (pair, u, n2) folds the bins v = n2 + NB e (e < NA) of row u for both paths
+// of the pair straight into registers, runs the DFT-NA and the twiddles W^(n2 k) and stores the
+// stage-A result in place of the batch rows (B is never written by a separate fold pass and read
+// back).  Offsets relative to the unit's bases are compile-time immediates: direct
+// db + (NB e) (+ N2 HLD for a = 1), mirrored mb + NB (NA-1-e) (+ N2 HLD for a = 0) with mb at the
+// unit's largest column, filters fo + NB e (+ N2 N1 / N2 / N2 N1 + N2).  Stage B follows after a
+// barrier (fft_lines_dr_stageB).
+template <int N1>
+__device__ __forceinline__ void fold2_s2_rowA(const float2* __restrict__ H, const float2* __restrict__ psi2,
+                                              int npair, int npath, float2* __restrict__ B,
+                                              const float2* __restrict__ tw) {
+    constexpr int N2 = N1 / 2, HLD = N1 / 2 + 1, LD2 = N2 | 1, PSLOT = N2 * LD2, PST = N1 * N1;
+    using F = wstfft::LineFFT<N2, true>;
+    static_assert(F::N2 > 1, "two-stage row sizes only");
+    constexpr int NA = F::N1, NB = F::N2, UNITS = N2 * NB;
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, npair * PST * 8);
+    const char* Hb = reinterpret_cast<const char*>(H);
+    // opaque start index: keeps the compiler from hoisting the unit's bases and twiddles out of
+    // the caller's batch loop (live across the whole level, they pushed k_o2 into spills)
+    int w0 = threadIdx.x;
+    asm volatile("" : "+v"(w0));
+    for (int w = w0; w < npair * UNITS; w += blockDim.x) {
+        const int pr = w / UNITS;
+        const int r = w - pr * UNITS;
+        const int u = r / NB, n2 = r - u * NB;
+        const int db = (u * HLD + n2) * 8;
+        const int mb = ((N2 - u) * HLD + (NB - n2)) * 8;
+        const int fo = (u * N1 + n2 + pr * PST) * 8;   // lanes of a wave may straddle pairs
+        float2 x0[NA], x1[NA];
+        wstfft::static_for<0, NA>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            constexpr int dv = NB * e, dm = NB * (NA - 1 - e);
+            const float2 h0 = lds_at(Hb, db + dv * 8), h1 = lds_at(Hb, db + (N2 * HLD + dv) * 8);
+            const float2 m0 = lds_at(Hb, mb + (N2 * HLD + dm) * 8), m1 = lds_at(Hb, mb + dm * 8);
+            const float2 f0 = buf_load2(rs, fo, dv * 8), f1 = buf_load2(rs, fo, (N2 * N1 + dv) * 8);
+            const float2 g0 = buf_load2(rs, fo, (N2 + dv) * 8);
+            const float2 g1 = buf_load2(rs, fo, (N2 * N1 + N2 + dv) * 8);
+            x0[e].x = fmaf(h0.x, f0.x, fmaf(h1.x, f1.x, fmaf(m0.x, g0.x, m1.x * g1.x)));
+            x0[e].y = fmaf(h0.y, f0.x, fmaf(h1.y, f1.x, fmaf(-m0.y, g0.x, -m1.y * g1.x)));
+            x1[e].x = fmaf(h0.x, f0.y, fmaf(h1.x, f1.y, fmaf(m0.x, g0.y, m1.x * g1.y)));
+            x1[e].y = fmaf(h0.y, f0.y, fmaf(h1.y, f1.y, fmaf(-m0.y, g0.y, -m1.y * g1.y)));
+            // pin both paths' sums here: sunk to their DFTs, the other path's filter values stayed
+            // live (spilled) across the first path's transform
+            asm volatile("" : "+v"(x0[e].x), "+v"(x0[e].y), "+v"(x1[e].x), "+v"(x1[e].y));
+            // at most WST_FUSE_GRP elements' loads in flight (register budget of 4 waves per SIMD)
+            if constexpr ((e + 1) % WST_FUSE_GRP == 0) __builtin_amdgcn_sched_barrier(0);
+        });
+        wstfft::rfft<NA, true>(x0);
+        wstfft::rfft<NA, true>(x1);
+        wstfft::static_for<1, NA>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            const float2 t = tw[n2 * k];
+            x0[k] = wstfft::cmul_tw(x0[k], t, true);
+            x1[k] = wstfft::cmul_tw(x1[k], t, true);
+        });
+        float2* d = B + 2 * pr * PSLOT + u * LD2 + n2;
+        wstfft::static_for<0, NA>([&](auto ec) {
+            constexpr int e = decltype(ec)::value;
+            d[NB * e] = x0[e];
+        });
+        if (2 * pr + 1 < npath)
+            wstfft::static_for<0, NA>([&](auto ec) {
+                constexpr int e = decltype(ec)::value;
+                d[PSLOT + NB * e] = x1[e];
+            });
+    }
+}
+
+// s = 4 / 8: per (pair, tile) header {first tap, direct groups, mirrored groups} and tap lists
+// padded to groups of four with dummy taps (LDS offset 0, filter offset into the zero block past
+// the filters), so four taps are in flight per group with no per-tap test.
+template <int N1, int S>
+__device__ __forceinline__ void fold2_tile_list(const float2* __restrict__ H, const float2* __restrict__ psi2,
+                                                int npair, int npath, float2* __restrict__ B,
+                                                const int4* __restrict__ hdr, const int2* __restrict__ taps) {
+    constexpr int N2 = N1 / S, HLD = N1 / 2 + 1, LD2 = N2 | 1, PSLOT = N2 * LD2;
+    constexpr int ITEMS = N2 * N2, NT = (ITEMS + 63) / 64, PST = N1 * N1;
+    const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, 0x7ffffff0);
+    const char* Hb = reinterpret_cast<const char*>(H);
+    const int w0 = wave_id();
+    for (int k = 0;; ++k) {
+        // wave-uniform tile index (readfirstlane: scalar loop control, pair and header offsets)
+        const int wi = __builtin_amdgcn_readfirstlane(w0 + k * nw);
+        if (wi >= npair * NT) break;
+        const int pr = wi / NT;
+        const int bin0 = (wi - pr * NT) * 64 + lane;
+        const int bin = min(bin0, ITEMS - 1);
+        const int u = bin / N2, v = bin - u * N2;
+        const int db = (u * HLD + v) * 8, mb = ((N2 - u) * HLD + (N2 - v)) * 8;
+        const int fo = (u * N1 + v) * 8, po = pr * PST * 8;
+        // header and tap lists through the constant address space: scalar loads into SGPRs
+        const cint_p hp = to_const_as(hdr) + 4 * wi;
+        const int ng_dir = hp[1], ng_mir = hp[2];
+        cint_p tl = to_const_as(taps) + 2 * hp[0];
+        float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+        for (int g = 0; g < ng_dir; ++g, tl += 8) {
+            float2 hv[4], fv[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                hv[c] = lds_at(Hb, db + tl[2 * c]);
+                fv[c] = buf_load2(rs, fo, tl[2 * c + 1] + po);
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                a0 = make_float2(fmaf(hv[c].x, fv[c].x, a0.x), fmaf(hv[c].y, fv[c].x, a0.y));
+                a1 = make_float2(fmaf(hv[c].x, fv[c].y, a1.x), fmaf(hv[c].y, fv[c].y, a1.y));
+            }
+        }
+        for (int g = 0; g < ng_mir; ++g, tl += 8) {
+            float2 hv[4], fv[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                hv[c] = lds_at(Hb, mb + tl[2 * c]);
+                fv[c] = buf_load2(rs, fo, tl[2 * c + 1] + po);
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                a0 = make_float2(fmaf(hv[c].x, fv[c].x, a0.x), fmaf(-hv[c].y, fv[c].x, a0.y));
+                a1 = make_float2(fmaf(hv[c].x, fv[c].y, a1.x), fmaf(-hv[c].y, fv[c].y, a1.y));
+            }
+        }
+        if (bin0 < ITEMS) {
+            float2* d = B + 2 * pr * PSLOT + u * LD2 + v;
+            d[0] = a0;
+            if (2 * pr + 1 < npath) d[PSLOT] = a1;
+        }
+    }
+}
+
 // XCD-aware decode of (plane, theta1) items: blocks b and b+8 share an XCD; give each XCD a
 // contiguous range so the L workgroups of a plane read its Xhat from one L2.
 __device__ __forceinline__ int xcd_item(int total) {
@@ -1362,15 +1603,32 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     const float2* X = xhat + static_cast<long long>(local) * PM * PN;
     const int b1 = p.box1_off[j1 * L + l1];
     const bool use_box1 = b1 >= 0 && (1 << j1) >= p.box1_min_s;
-    if (!(dbg & 128)) fold1_any(1 << j1, X, psi0, PN, A, ld1, nM1, nN1, use_box1 ? p.box + b1 : nullptr);
-    __syncthreads();
-
-    // 2. U1 = |ifft(.)|, modulus fused into the last pass; fold-mean + ifft scale = 1/(PM PN).
-    //    In place (digit-reversed rows and columns); the low-pass maps the permutation.
+    // square level-0 plane of a compile-time two-stage size: the product fused with the rows'
+    // stage A (fold1_rowA)
+    // (SQ geometry kernels: c2 k_o1 j1 = 0 0.778 -> 0.726 ms; the non-SQ 136^2 level of f3 measured
+    // 0.78 -> 0.79, so the exported-spectrum kernels keep the separate fold)
+    constexpr bool FUSE1 = SQ && N1C >= WST_FUSE1_MIN && wstfft::LineFFT<(N1C > 0 ? N1C : 2), true>::N2 > 1;
+    const bool fused1 = FUSE1 && j1 == 0;
     EpiModulus mod1{1.f / (static_cast<float>(PM) * static_cast<float>(PN)), 0.f};
-    if (!(dbg & 1))
-        lds_fft2<FM, FN, SQ ? prev_cap(MAXN) : 0, MAXN, kDR, true>(A, 1, 0, nM1, nN1, ld1, tb.twM(j1),
-                                                                  tb.twN(j1), mod1);
+    if (fused1) {
+        if constexpr (FUSE1) {
+            fold1_rowA<N1C>(X, psi0, A, tb.twN(j1));
+            __syncthreads();
+            wstfft::EpiIdentity id1;
+            wstfft::fft_lines_dr_stageB<N1C, true>(A, wstfft::Lines{1, 0, nM1, ld1, 1}, id1);
+            lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kDR, true>(A, wstfft::Lines{1, 0, nN1, 1, ld1}, nM1,
+                                                                       tb.twM(j1), mod1);
+        }
+    } else {
+        if (!(dbg & 128)) fold1_any(1 << j1, X, psi0, PN, A, ld1, nM1, nN1, use_box1 ? p.box + b1 : nullptr);
+        __syncthreads();
+
+        // 2. U1 = |ifft(.)|, modulus fused into the last pass; fold-mean + ifft scale = 1/(PM PN).
+        //    In place (digit-reversed rows and columns); the low-pass maps the permutation.
+        if (!(dbg & 1))
+            lds_fft2<FM, FN, SQ ? prev_cap(MAXN) : 0, MAXN, kDR, true>(A, 1, 0, nM1, nN1, ld1, tb.twM(j1),
+                                                                      tb.twN(j1), mod1);
+    }
     const float mean1 = block_sum(mod1.sum, red) / n1;
 
     // 3. S1 at level j1, decimation 2^(J-j1)
@@ -1559,6 +1817,11 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
         if (!(dbg & 4))
             lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(
                 Hl, wstfft::Lines{1, 0, hld, 1, hld}, nM1, tb.twM(j1), id);
+        if constexpr (N1C > 0) {
+            // row N1 = row 0: the tile folds' mirrored taps of bin row u = 0 at alias a = 0
+            for (int i = threadIdx.x; i < hld; i += blockDim.x) Hl[nM1 * hld + i] = Hl[i];
+            __syncthreads();
+        }
     }
 
     // 2. order-2 paths in batches: Hermitian fold -> |ifft| -> S2 low-pass
@@ -1566,8 +1829,13 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     const int nq = (L + 1) >> 1;
     int bctr = 0;   // batch counter (split HG launches)
     // every batch of paths of level j2 (sizes nM2 x nN2); PB > 0: compile-time paths per batch
-    auto level = [&](int j2, int nM2, int nN2, auto pbc) __attribute__((always_inline)) {
+    // SC > 0: the alias count s is a compile-time constant (square level N1C: tile-mapped folds)
+    auto level = [&](int j2, int nM2, int nN2, auto pbc, auto scc) __attribute__((always_inline)) {
         constexpr int PB = decltype(pbc)::value;
+        constexpr int SC = decltype(scc)::value;
+        // s = 2 fold fused with the rows' stage A (two-stage row sizes >= WST_FUSE_MIN)
+        constexpr bool FUSE = N1C > 0 && SC == 2 && N1C / 2 >= WST_FUSE_MIN &&
+                              wstfft::LineFFT<(N1C > 0 ? N1C / 2 : 2), true>::N2 > 1;
         const int ld2 = odd_ld(nN2);
         const int pslot = nM2 * ld2;
         const int s2 = 1 << (j2 - j1);
@@ -1584,16 +1852,32 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             const float2* ps = p.psi2 + p.psi2_off[(j2 * J + j1) * nq + (l2a >> 1)];
             const long long pstride = static_cast<long long>(n1);
             const int* bx = p.box + p.box_off[j2 * J + j1] + (l2a >> 1) * (nM2 + nN2);
-            if (!(dbg & 8) && !(dbg & (s2 == 2 ? 256 : 512)))
-                fold2_any<HG ? 2 : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2, nN2,
-                          bx, nM2 + nN2);
+            if (!(dbg & 8) && !(dbg & (s2 == 2 ? 256 : 512))) {
+                if constexpr (FUSE) {
+                    fold2_s2_rowA<N1C>(H, ps, npair, npath, B, tb.twN(j2));
+                } else if constexpr (N1C > 0 && SC == 2) {
+                    fold2_tile_s2<N1C>(H, ps, npair, npath, B);
+                } else if constexpr (N1C > 0 && (SC == 4 || SC == 8)) {
+                    constexpr int NT = ((N1C / SC) * (N1C / SC) + 63) / 64;
+                    fold2_tile_list<N1C, SC>(H, ps, npair, npath, B,
+                                             p.taph + p.taph_off[j2 * J + j1] + (l2a >> 1) * NT, p.taps);
+                } else {
+                    fold2_any<HG ? 2 : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2,
+                                          nN2, bx, nM2 + nN2);
+                }
+            }
             __syncthreads();
             const float scale2 = 1.f / static_cast<float>(n1);
             if constexpr (SQ) {
                 // rows, then the column pass fused with |.| and the S2 low-pass
-                if (!(dbg & 16))
-                    lds_fft_lines<FN, 0, PHI, kDR, true>(
-                        B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, nN2, tb.twN(j2), id);
+                if (!(dbg & 16)) {
+                    if constexpr (FUSE)
+                        wstfft::fft_lines_dr_stageB<(N1C > 0 ? N1C / 2 : 2), true>(
+                            B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, id);
+                    else
+                        lds_fft_lines<FN, 0, PHI, kDR, true>(
+                            B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, nN2, tb.twN(j2), id);
+                }
                 const int k0 = kbase + (j2 - j1 - 1) * L + l2a;
                 float* outd = pooled ? nullptr : out + (img * p.K + k0) * (oM * oN);
                 if (!(dbg & 64))
@@ -1634,7 +1918,8 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             constexpr int NN2 = N1C >> k;
             if constexpr ((NN2 << k) == N1C && NN2 >= 1)
                 if (j1 + k < J && j1 + k >= j2first)
-                    level(j1 + k, NN2, NN2, std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{});
+                    level(j1 + k, NN2, NN2, std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
+                          std::integral_constant<int, (1 << k)>{});
         });
     } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {
         // after a big level the paths start at the first LDS-resident level, which is the
@@ -1646,10 +1931,10 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                 constexpr int k = decltype(kc)::value;
                 constexpr int NN2 = N2C >> k;
                 if constexpr ((NN2 << k) == N2C && NN2 >= 1)
-                    if (j2first + k < J) level(j2first + k, NN2, NN2, std::integral_constant<int, 0>{});
+                    if (j2first + k < J) level(j2first + k, NN2, NN2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
             });
         } else {
-            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{});
+            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
         }
     } else if constexpr (!SQ && HG == 1 && FM == FN && FM > 0) {
         // exported-spectrum k_o2 (f3 / c1): a square level of one of the family's sizes in this
@@ -1667,16 +1952,17 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                             if constexpr ((NN2 << k) == N1X && NN2 >= 1)
                                 if (j1 + k < J)
                                     level(j1 + k, NN2, NN2,
-                                          std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{});
+                                          std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
+                                          std::integral_constant<int, 0>{});
                         });
                     }
                 }
             });
         }
         if (!done)
-            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{});
+            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
     } else {
-        for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{});
+        for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
     }
 }
 

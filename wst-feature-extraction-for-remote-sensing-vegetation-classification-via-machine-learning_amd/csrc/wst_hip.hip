@@ -154,6 +154,9 @@ struct wst_plan {
     int* d_box = nullptr;
     int* d_box_off = nullptr;
     int* d_box1_off = nullptr;
+    int* d_taph = nullptr;
+    int* d_taph_off = nullptr;
+    int* d_taps = nullptr;
     std::vector<long long> psi2_off_host;
     std::vector<int> box_off_host;
     float* d_lpt = nullptr;
@@ -231,6 +234,9 @@ void free_plan(wst_plan* p) {
     (void)hipFree(p->d_box);
     (void)hipFree(p->d_box_off);
     (void)hipFree(p->d_box1_off);
+    (void)hipFree(p->d_taph);
+    (void)hipFree(p->d_taph_off);
+    (void)hipFree(p->d_taps);
     (void)hipFree(p->d_lpt);
     (void)hipFree(p->d_lpt_off);
     (void)hipFree(p->d_lpn);
@@ -556,6 +562,70 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                 }
             }
     }
+    // tile tap lists of the square order-2 folds at s = 4 / 8 (wst_device.h fold2_tile_list): per
+    // (j2, r) and pair q the N2^2 bins in tiles of 64; a tile's list holds every alias (a, b) at
+    // which some bin of the tile meets a bin where either filter of the pair exceeds kBoxThreshold
+    // of its maximum (every tap the box fold keeps at that bin), direct (b < s/2) then mirrored,
+    // each padded to groups of four with dummy taps that read the zero block appended to psi2.
+    std::vector<int> taph, taps;
+    std::vector<int> taph_off(static_cast<size_t>(J) * J, 0);
+    size_t psi2_zero = 0;   // float2 index of the zero block (dummy taps)
+    if (max_order >= 2 && g.PM == g.PN) {
+        psi2_zero = psi2.size();
+        psi2.resize(psi2.size() + static_cast<size_t>(g.PM) * g.PM / 2 + 64, make_float2(0.f, 0.f));
+        for (int j2 = 1; j2 < J; ++j2)
+            for (int r = 0; r < j2 && r < wst::psi_levels(j2, J); ++r) {
+                const int S = 1 << (j2 - r), N1 = g.PM >> r, N2 = g.PM >> j2, HLD = N1 / 2 + 1;
+                if (S < 4 || S > 8) continue;
+                const int items = N2 * N2, nt = (items + 63) / 64;
+                taph_off[static_cast<size_t>(j2) * J + r] = static_cast<int>(taph.size() / 4);
+                for (int q = 0; q < nq; ++q) {
+                    const long long fbase = psi2_off[(static_cast<size_t>(j2) * J + r) * nq + q];
+                    std::vector<char> sig(static_cast<size_t>(N1) * N1, 0);
+                    for (int u = 0; u < 2; ++u) {
+                        const int l2 = 2 * q + u;
+                        if (l2 >= L) continue;
+                        const auto& f = fb.psi[static_cast<size_t>(j2) * L + l2][r];
+                        double mx = 0.0;
+                        for (double v : f) mx = std::max(mx, std::fabs(v));
+                        for (size_t i = 0; i < f.size(); ++i)
+                            if (std::fabs(f[i]) > kBoxThreshold * mx) sig[i] = 1;
+                    }
+                    for (int t = 0; t < nt; ++t) {
+                        std::vector<int> dir, mir;
+                        for (int a = 0; a < S; ++a)
+                            for (int b = 0; b < S; ++b) {
+                                bool hit = false;
+                                for (int bin = 64 * t; bin < std::min(items, 64 * t + 64) && !hit; ++bin) {
+                                    const int u = bin / N2, v = bin % N2;
+                                    hit = sig[static_cast<size_t>(u + N2 * a) * N1 + v + N2 * b] != 0;
+                                }
+                                if (!hit) continue;
+                                const int fo = (N2 * a * N1 + N2 * b) * 8;
+                                if (b < S / 2) {
+                                    dir.push_back((N2 * a * HLD + N2 * b) * 8);
+                                    dir.push_back(fo);
+                                } else {
+                                    mir.push_back((N2 * (S - 1 - a) * HLD + N2 * (S - 1 - b)) * 8);
+                                    mir.push_back(fo);
+                                }
+                            }
+                        const int dummy = static_cast<int>((static_cast<long long>(psi2_zero) - fbase) * 8);
+                        for (auto* lst : {&dir, &mir})
+                            while (lst->size() % 8) {
+                                lst->push_back(0);
+                                lst->push_back(dummy);
+                            }
+                        taph.push_back(static_cast<int>(taps.size() / 2));
+                        taph.push_back(static_cast<int>(dir.size() / 8));
+                        taph.push_back(static_cast<int>(mir.size() / 8));
+                        taph.push_back(0);
+                        taps.insert(taps.end(), dir.begin(), dir.end());
+                        taps.insert(taps.end(), mir.begin(), mir.end());
+                    }
+                }
+            }
+    }
     // order-1 alias boxes (psi_{j,l} at level 0 folded by s = 2^j; s >= 4 only)
     std::vector<int> box1_off(static_cast<size_t>(J) * L, -1);
     for (int j = 2; j < J; ++j)
@@ -704,6 +774,9 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     if ((rc = upload(&plan->d_box, box)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_box_off, box_off)) != WST_OK) return rc;
     if ((rc = upload(&plan->d_box1_off, box1_off)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_taph, taph)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_taph_off, taph_off)) != WST_OK) return rc;
+    if ((rc = upload(&plan->d_taps, taps)) != WST_OK) return rc;
     plan->psi2_off_host = psi2_off;
     plan->box_off_host = box_off;
     if ((rc = upload(&plan->d_lpt, lpt)) != WST_OK) return rc;
@@ -729,6 +802,9 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     dp.o2_base = plan->d_o2;
     dp.psi2 = plan->d_psi2; dp.psi2_off = plan->d_psi2_off;
     dp.box = plan->d_box; dp.box_off = plan->d_box_off; dp.box1_off = plan->d_box1_off;
+    dp.taph = reinterpret_cast<const int4*>(plan->d_taph);
+    dp.taph_off = plan->d_taph_off;
+    dp.taps = reinterpret_cast<const int2*>(plan->d_taps);
     // the order-1 box-sparse fold pays off from s = 8 on (measured on MI355X at c2); order 2
     // uses it for every s >= 4
     dp.box1_min_s = 8;
@@ -918,8 +994,9 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         size_t smax = 0;
         for (int j2 = j1 + 1; j2 < J; ++j2)
             smax = std::max(smax, static_cast<size_t>(paths_per_batch(bcap, pslot(j2), L)) * omn);
-        if (plan->sq)   // tap matrices replace the 1-D taps and permutations; M-side tables only
-            plan->o2_lds[j1] = layout(plan->o2_lay[j1], static_cast<size_t>(nM1) * hld * sizeof(float2),
+        if (plan->sq)   // tap matrices replace the 1-D taps and permutations; M-side tables only;
+                        // H holds row nM1 = row 0 (the tile folds' mirrored taps)
+            plan->o2_lds[j1] = layout(plan->o2_lay[j1], static_cast<size_t>(nM1 + 1) * hld * sizeof(float2),
                                       bcap * sizeof(float2), t, Blocks{j1, J - 1, false}, 1, 0, smax,
                                       Blocks{j1 + 1, J - 1, false}, oms);
         else
@@ -993,6 +1070,10 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         if (plan->o2_lds[j1] > 0) plan->o2_threads[j1] = fill_cu(plan->o2_threads[j1], plan->o2_lds[j1], 768);
     }
     if (plan->rb == 0) plan->prep_threads = fill_cu(static_cast<int>(plan->prep_threads), plan->prep_lds);
+#ifdef WST_O2T0   // A/B build: k_o2 workgroup size at the SQ 96^2 class
+    for (int j1 = plan->rb; j1 < J; ++j1)
+        if (plan->sq && plan->cap[j1] == 136 && plan->o2_lds[j1] > 0) plan->o2_threads[j1] = WST_O2T0;
+#endif
     threads_override("WST_O1_THREADS", plan->o1_threads);
     threads_override("WST_O2_THREADS", plan->o2_threads);
     threads_override("WST_O2X_THREADS", plan->o2x_threads);
