@@ -109,11 +109,17 @@ struct LdsLayout {
                             // b % nsplit; one item's workgroups share an XCD (its L2 holds H)
     int hgroup;             // k_o2 HG split: items per dispatch group of an XCD; within a group
                             // the slots run batch-major (one batch of hgroup items, then the next)
+    int hext;               // resident levels: an item's half spectrum in the workspace holds
+                            // nM1 + 1 rows (row nM1 = row 0 for the tile folds' mirrored taps;
+                            // written by an exporting k_o1, formed in LDS by k_o2 otherwise)
 };
 
 // ------------------------------------------------------------------------------------------
 // helpers
 // ------------------------------------------------------------------------------------------
+// wave index within the workgroup as a provably uniform (scalar) value
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 __device__ __forceinline__ int reflect_index(int i, int n) {
     // numpy.pad(mode='reflect') for any pad width: even periodic extension, period 2(n-1)
     if (n == 1) return 0;
@@ -609,6 +615,136 @@ __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int 
     }
     __syncthreads();
 }
+
+// Register-cached MFMA low-pass of square K x K arrays (K compile-time): the tap operands of a
+// whole tile (every K step: KS floats per lane) are loaded once per wave and call -- step 1 fixes a
+// wave's column tile (nt = wave % nnt) for all of its (b, row-tile) tasks, step 2's operands are
+// issued at entry, behind step 1 -- instead of once per 8 K steps of every task (the L2 latency of
+// the tap loads, not the matrix pipe, bounded the phase).  Same operand order, K parts and results
+// as lds_lowpass_mfma.  Needs nw % nnt == 0.  Ends with a barrier.
+constexpr int mfma_k_steps(int k) {
+    return 16 * (k / 64) + 4 * ((k % 64) / 16) + ((k % 16) + 3) / 4;
+}
+template <int K>
+__device__ __forceinline__ void lds_lowpass_mfma_rc(float2* U, int nb, int bs, int ld,
+                                                    const float* __restrict__ GM,
+                                                    const float* __restrict__ GN, int oMp, int oNp,
+                                                    int oM, int oN, float* S, int s_bs = -1, int s_es = 1) {
+    constexpr int N64 = K / 64, N16 = (K % 64) / 16, NTL = ((K % 16) + 3) / 4;
+    constexpr int KS = mfma_k_steps(K), NMT = (K + 15) / 16, Q16 = 64 * N64, QT = 64 * N64 + 16 * N16;
+    if (s_bs < 0) s_bs = oM * oN;
+    const int lane = threadIdx.x & 63, wave = wave_id(), nw = blockDim.x >> 6;
+    const int li = lane & 15, lk = lane >> 4;
+    const int nnt = oNp >> 4, nat = oMp >> 4;
+    // lane's operand of every K step of tile t of a tap matrix with ntile column tiles
+    auto load_ops = [&](const float* G, int ntile, int t, float (&g)[KS]) __attribute__((always_inline)) {
+        const float4* g64 = reinterpret_cast<const float4*>(G) + (t * 64 + lane) * 4;
+        wstfft::static_for<0, N64>([&](auto bc) {
+            constexpr int blk = decltype(bc)::value;
+            wstfft::static_for<0, 4>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                const float4 v = g64[blk * ntile * 256 + j];
+                g[16 * blk + 4 * j] = v.x;
+                g[16 * blk + 4 * j + 1] = v.y;
+                g[16 * blk + 4 * j + 2] = v.z;
+                g[16 * blk + 4 * j + 3] = v.w;
+            });
+        });
+        const float4* g16 = reinterpret_cast<const float4*>(G) + N64 * ntile * 256 + t * 64 + lane;
+        wstfft::static_for<0, N16>([&](auto bc) {
+            constexpr int blk = decltype(bc)::value;
+            const float4 v = g16[blk * ntile * 64];
+            g[16 * N64 + 4 * blk] = v.x;
+            g[16 * N64 + 4 * blk + 1] = v.y;
+            g[16 * N64 + 4 * blk + 2] = v.z;
+            g[16 * N64 + 4 * blk + 3] = v.w;
+        });
+        const float* gcol = G + (N64 * 4 + N16) * ntile * 256 - QT * (ntile * 16) + t * 16 + li;
+        wstfft::static_for<0, NTL>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            const int q = QT + 4 * s + lk;
+            g[16 * N64 + 4 * N16 + s] = q < K ? gcol[q * (ntile * 16)] : 0.f;
+        });
+    };
+    // row / column index of K step s for this lane
+    auto kidx = [&](auto sc) __attribute__((always_inline)) {
+        constexpr int s = decltype(sc)::value;
+        if constexpr (s < 16 * N64) return 64 * (s / 16) + (s % 16) + 16 * lk;
+        else if constexpr (s < 16 * N64 + 4 * N16) return Q16 + 16 * ((s - 16 * N64) / 4) + 4 * ((s - 16 * N64) % 4) + lk;
+        else return QT + 4 * (s - 16 * N64 - 4 * N16) + lk;
+    };
+    float g2[KS];
+    const int t2_0 = wave;   // first step-2 task of this wave
+    int at2 = -1;
+    if (t2_0 < nb * nat * nnt) {
+        at2 = (t2_0 % (nat * nnt)) / nnt;
+        load_ops(GM, nat, at2, g2);
+    }
+    // 1. T = U GN
+    {
+        float g[KS];
+        const int nt = wave % nnt;
+        load_ops(GN, nnt, nt, g);
+        for (int tk = wave / nnt; tk < nb * NMT; tk += nw / nnt) {
+            const int b = tk / NMT, mt = tk - b * NMT;
+            float2* Ub = U + b * bs;
+            const int p = mt * 16 + li;
+            const bool pok = p < K;
+            const float2* urow = Ub + (pok ? p : K - 1) * ld;
+            f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+            wstfft::static_for<0, KS>([&](auto sc) {
+                constexpr int s = decltype(sc)::value;
+                const int q = kidx(sc);
+                float a = lds_half64(urow + (s >= 16 * N64 + 4 * N16 ? (q < K ? q : 0) : q), 0);
+                if constexpr (s >= 16 * N64 + 4 * N16) a = q < K ? a : 0.f;
+                a = pok ? a : 0.f;
+                if constexpr (s % 2 == 0) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g[s], acc0, 0, 0, 0);
+                else acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, g[s], acc1, 0, 0, 0);
+            });
+            const int c = nt * 16 + li;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int pp = mt * 16 + lk * 4 + i;
+                if (pp < K && c < oN) Ub[pp * ld + c].y = acc0[i] + acc1[i];
+            }
+        }
+    }
+    __syncthreads();
+    // 2. S = GM^T T
+    for (int t = wave; t < nb * nat * nnt; t += nw) {
+        const int b = t / (nat * nnt);
+        const int r = t - b * nat * nnt;
+        const int at = r / nnt, ct = r - at * nnt;
+        if (at != at2) {
+            at2 = at;
+            load_ops(GM, nat, at, g2);
+        }
+        const float2* Ub = U + b * bs;
+        const int c = ct * 16 + li;
+        const bool cok = c < oN;
+        f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        wstfft::static_for<0, KS>([&](auto sc) {
+            constexpr int s = decltype(sc)::value;
+            const int p = kidx(sc);
+            const int pc = (s >= 16 * N64 + 4 * N16 && p >= K) ? 0 : p;
+            float bv = lds_half64(Ub + pc * ld + (cok ? c : 0), 1);
+            if constexpr (s >= 16 * N64 + 4 * N16) bv = p < K ? bv : 0.f;
+            bv = cok ? bv : 0.f;
+            if constexpr (s % 2 == 0) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(g2[s], bv, acc0, 0, 0, 0);
+            else acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(g2[s], bv, acc1, 0, 0, 0);
+        });
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int a_ = at * 16 + lk * 4 + i;
+            if (a_ < oM && cok) S[b * s_bs + (a_ * oN + c) * s_es] = acc0[i] + acc1[i];
+        }
+    }
+    __syncthreads();
+}
+
+// register-cached form for compile-time square sizes with at most 18 K steps (72^2, 68^2, 36^2 ...)
+template <int K>
+constexpr bool mfma_rc_ok() { return K > 0 && mfma_k_steps(K) <= 18; }
 
 __device__ __forceinline__ bool wide_lowpass(const DevParams& p) { return p.oM > kLpOM || p.oN > kLpOM; }
 __device__ __forceinline__ const float* lpw_M(const DevParams& p, int slot) { return p.lpw + p.lpw_off[2 * slot]; }
@@ -1287,7 +1423,6 @@ __device__ __forceinline__ void fold2_any(int s2, const float2* H, int hld, int 
 __device__ __forceinline__ float2 lds_at(const char* base, int byte_off) {
     return *reinterpret_cast<const float2*>(base + byte_off);
 }
-__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 // read-only table in the constant address space: loads at wave-uniform addresses become s_load
 typedef const __attribute__((address_space(4))) int* cint_p;
 template <typename T>
@@ -1516,7 +1651,12 @@ __device__ __forceinline__ void prep_body(unsigned char* smem, const DevParams& 
 
     // S0: low-pass at level 0, decimation 2^J
     if (wide_lowpass(p))   // natural-order level-0 tap matrices (slot J)
-        lds_lowpass_mfma(A, 1, 0, PM, PN, ld, lpw_M(p, p.J), lpw_N(p, p.J), p.oMp, p.oNp, p.oM, p.oN, S);
+    {
+        if constexpr (mfma_rc_ok<PC>())
+            lds_lowpass_mfma_rc<PC>(A, 1, 0, ld, lpw_M(p, p.J), lpw_N(p, p.J), p.oMp, p.oNp, p.oM, p.oN, S);
+        else
+            lds_lowpass_mfma(A, 1, 0, PM, PN, ld, lpw_M(p, p.J), lpw_N(p, p.J), p.oMp, p.oNp, p.oM, p.oN, S);
+    }
     else
         lds_lowpass(A, 1, 0, PM, PN, ld, tb.lpM(0), tb.lpN(0), nullptr, nullptr, 1 << p.J, p.oM, p.oN, S);
     emit(S, 1, 0, img, p.K, p.oM, p.oN, out, pooled);
@@ -1637,8 +1777,13 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
         if constexpr (SQ)
             lds_lowpass_taps<8, 16>(A, nM1, nN1, ld1, tb.gM(j1), tb.gN(j1), oms, oM, oN, S);
         else if (wide_lowpass(p))
-            lds_lowpass_mfma(A, 1, 0, nM1, nN1, ld1, lpw_M(p, j1), lpw_N(p, j1), p.oMp, p.oNp, oM,
-                             oN, S);
+        {
+            if constexpr (mfma_rc_ok<N1C>())
+                lds_lowpass_mfma_rc<N1C>(A, 1, 0, ld1, lpw_M(p, j1), lpw_N(p, j1), p.oMp, p.oNp, oM, oN, S);
+            else
+                lds_lowpass_mfma(A, 1, 0, nM1, nN1, ld1, lpw_M(p, j1), lpw_N(p, j1), p.oMp, p.oNp, oM,
+                                 oN, S);
+        }
         else
             lds_lowpass(A, 1, 0, nM1, nN1, ld1, tb.lpM(j1), tb.lpN(j1), tb.pmM(j1), tb.pmN(j1),
                         1 << (J - j1), oM, oN, S);
@@ -1660,7 +1805,7 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
 
     // 5. split into the two rows' half spectra (columns 0..nN1/2) and export them
     const int hld = (nN1 >> 1) + 1;
-    float2* H = hexp + static_cast<long long>(item) * nM1 * hld;
+    float2* H = hexp + static_cast<long long>(item) * (nM1 + lay.hext) * hld;
     if (lay.export_full) {
         // in place: packed row 2t -> half-spectrum rows 2t and 2t+1 (the odd rows of A are free),
         // then the column FFTs (rows digit-reversed -> natural); k_o2 folds the fully transformed
@@ -1695,6 +1840,8 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
         lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(A, wstfft::Lines{1, 0, hld, 1, ld1}, nM1,
                                                                      tb.twM(j1), id);
         for (GridIter it(hld); it.u < nM1; it.next()) stnt(H + it.u * hld + it.v, A[it.u * ld1 + it.v]);
+        if (lay.hext)
+            for (int i = threadIdx.x; i < hld; i += blockDim.x) stnt(H + nM1 * hld + i, A[i]);
         return;
     }
     for (GridIter it(hld); it.u < nh; it.next()) {
@@ -1798,7 +1945,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     const int nM1 = N1C ? N1C : PM >> j1, nN1 = N1C ? N1C : PN >> j1;
     const int n1 = nM1 * nN1;
     const int hld = (nN1 >> 1) + 1;
-    const float2* Hg = hexp + static_cast<long long>(item) * nM1 * hld;
+    const float2* Hg = hexp + static_cast<long long>(item) * (nM1 + lay.hext) * hld;
     const float2* H = HG ? Hg : reinterpret_cast<const float2*>(smem);
     float2* B = reinterpret_cast<float2*>(smem + lay.off_b);
     float* S = reinterpret_cast<float*>(smem + lay.off_s);
@@ -1830,12 +1977,17 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     int bctr = 0;   // batch counter (split HG launches)
     // every batch of paths of level j2 (sizes nM2 x nN2); PB > 0: compile-time paths per batch
     // SC > 0: the alias count s is a compile-time constant (square level N1C: tile-mapped folds)
-    auto level = [&](int j2, int nM2, int nN2, auto pbc, auto scc) __attribute__((always_inline)) {
+    // NC > 0: the (square) path size is a compile-time constant
+    auto level = [&](int j2, int nM2, int nN2, auto pbc, auto scc, auto ncc) __attribute__((always_inline)) {
         constexpr int PB = decltype(pbc)::value;
         constexpr int SC = decltype(scc)::value;
+        constexpr int NC = decltype(ncc)::value;
         // s = 2 fold fused with the rows' stage A (two-stage row sizes >= WST_FUSE_MIN)
-        constexpr bool FUSE = N1C > 0 && SC == 2 && N1C / 2 >= WST_FUSE_MIN &&
-                              wstfft::LineFFT<(N1C > 0 ? N1C / 2 : 2), true>::N2 > 1;
+        // N1F > 0: the spectrum's (square) size at compile time -- tile-mapped folds, reading H from
+        // LDS or, in the exported-spectrum SQ kernel (HG), from HBM / L2 with the same offsets
+        constexpr int N1F = (SQ && NC > 0 && SC > 0) ? NC * SC : 0;
+        constexpr bool FUSE = N1F > 0 && SC == 2 && N1F / 2 >= WST_FUSE_MIN &&
+                              wstfft::LineFFT<(N1F > 0 ? N1F / 2 : 2), true>::N2 > 1;
         const int ld2 = odd_ld(nN2);
         const int pslot = nM2 * ld2;
         const int s2 = 1 << (j2 - j1);
@@ -1854,12 +2006,12 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             const int* bx = p.box + p.box_off[j2 * J + j1] + (l2a >> 1) * (nM2 + nN2);
             if (!(dbg & 8) && !(dbg & (s2 == 2 ? 256 : 512))) {
                 if constexpr (FUSE) {
-                    fold2_s2_rowA<N1C>(H, ps, npair, npath, B, tb.twN(j2));
-                } else if constexpr (N1C > 0 && SC == 2) {
-                    fold2_tile_s2<N1C>(H, ps, npair, npath, B);
-                } else if constexpr (N1C > 0 && (SC == 4 || SC == 8)) {
-                    constexpr int NT = ((N1C / SC) * (N1C / SC) + 63) / 64;
-                    fold2_tile_list<N1C, SC>(H, ps, npair, npath, B,
+                    fold2_s2_rowA<N1F>(H, ps, npair, npath, B, tb.twN(j2));
+                } else if constexpr (N1F > 0 && SC == 2) {
+                    fold2_tile_s2<N1F>(H, ps, npair, npath, B);
+                } else if constexpr (N1F > 0 && (SC == 4 || SC == 8)) {
+                    constexpr int NT = ((N1F / SC) * (N1F / SC) + 63) / 64;
+                    fold2_tile_list<N1F, SC>(H, ps, npair, npath, B,
                                              p.taph + p.taph_off[j2 * J + j1] + (l2a >> 1) * NT, p.taps);
                 } else {
                     fold2_any<HG ? 2 : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2,
@@ -1872,7 +2024,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                 // rows, then the column pass fused with |.| and the S2 low-pass
                 if (!(dbg & 16)) {
                     if constexpr (FUSE)
-                        wstfft::fft_lines_dr_stageB<(N1C > 0 ? N1C / 2 : 2), true>(
+                        wstfft::fft_lines_dr_stageB<(N1F > 0 ? N1F / 2 : 2), true>(
                             B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, id);
                     else
                         lds_fft_lines<FN, 0, PHI, kDR, true>(
@@ -1896,8 +2048,12 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                         // the maps go to the .x slots of the arrays (no S region: the exported-
                         // spectrum k_o2 fits two workgroups per CU); the next fold rewrites B
                         float* SB = reinterpret_cast<float*>(B);
-                        lds_lowpass_mfma(B, npath, pslot, nM2, nN2, ld2, lpw_M(p, j2), lpw_N(p, j2),
-                                         p.oMp, p.oNp, oM, oN, SB, 2 * pslot, 2);
+                        if constexpr (mfma_rc_ok<NC>())
+                            lds_lowpass_mfma_rc<NC>(B, npath, pslot, ld2, lpw_M(p, j2), lpw_N(p, j2), p.oMp,
+                                                    p.oNp, oM, oN, SB, 2 * pslot, 2);
+                        else
+                            lds_lowpass_mfma(B, npath, pslot, nM2, nN2, ld2, lpw_M(p, j2), lpw_N(p, j2),
+                                             p.oMp, p.oNp, oM, oN, SB, 2 * pslot, 2);
                         if (!(dbg & 2048)) emit(SB, npath, k0, img, p.K, oM, oN, out, pooled, 2 * pslot, 2);
                         __syncthreads();
                     } else {
@@ -1919,22 +2075,35 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             if constexpr ((NN2 << k) == N1C && NN2 >= 1)
                 if (j1 + k < J && j1 + k >= j2first)
                     level(j1 + k, NN2, NN2, std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
-                          std::integral_constant<int, (1 << k)>{});
+                          std::integral_constant<int, (1 << k)>{}, std::integral_constant<int, NN2>{});
         });
     } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {
         // after a big level the paths start at the first LDS-resident level, which is the
         // family's single size of this class (> 136 / 2): compile-time sizes from there on
         // (runtime sizes when a plan stages that level too and starts further down)
         constexpr int N2C = unique_level(FM, MAXN);
-        if ((PM >> j2first) == N2C) {
+        if (j2first == j1 + 1 && (PM >> j1) == N2C && PM == PN) {
+            // exported spectrum of a resident level of the class's single size (k_o1 finished
+            // the column FFTs): compile-time path sizes N2C / 2^k and tile-mapped folds from HBM
+            wstfft::static_for<1, 8>([&](auto kc) {
+                constexpr int k = decltype(kc)::value;
+                constexpr int NN2 = N2C >> k;
+                if constexpr ((NN2 << k) == N2C && NN2 >= 1)
+                    if (j1 + k < J)
+                        level(j1 + k, NN2, NN2, std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
+                              std::integral_constant<int, (1 << k)>{}, std::integral_constant<int, NN2>{});
+            });
+        } else if ((PM >> j2first) == N2C) {
             wstfft::static_for<0, 8>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
                 constexpr int NN2 = N2C >> k;
                 if constexpr ((NN2 << k) == N2C && NN2 >= 1)
-                    if (j2first + k < J) level(j2first + k, NN2, NN2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+                    if (j2first + k < J) level(j2first + k, NN2, NN2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+                  std::integral_constant<int, 0>{});
             });
         } else {
-            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+                  std::integral_constant<int, 0>{});
         }
     } else if constexpr (!SQ && HG == 1 && FM == FN && FM > 0) {
         // exported-spectrum k_o2 (f3 / c1): a square level of one of the family's sizes in this
@@ -1953,16 +2122,18 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                                 if (j1 + k < J)
                                     level(j1 + k, NN2, NN2,
                                           std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
-                                          std::integral_constant<int, 0>{});
+                                          std::integral_constant<int, 0>{}, std::integral_constant<int, NN2>{});
                         });
                     }
                 }
             });
         }
         if (!done)
-            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+                  std::integral_constant<int, 0>{});
     } else {
-        for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+        for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+                  std::integral_constant<int, 0>{});
     }
 }
 
@@ -1974,7 +2145,7 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     if constexpr (SQ) {
         if (p.oM == 4 && p.oN == 4 && lay.oms == 4) {
-            if constexpr (!HG && unique_level(FM, MAXN) > 0) {
+            if constexpr (unique_level(FM, MAXN) > 0) {
                 if (p.L == 8) {
                     k_o2_body<FM, FN, MAXN, SQ, HG, 4, 8>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
                     return;

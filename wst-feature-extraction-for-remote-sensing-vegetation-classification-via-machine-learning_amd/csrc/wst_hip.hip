@@ -987,7 +987,8 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
             return fail(WST_ERR_UNSUPPORTED, "order-2 level sizes must be even");
         const int hld = nN1 / 2 + 1;
         plan->ws_h_off[j1] = wsp;
-        wsp += static_cast<size_t>(L) * nM1 * hld * sizeof(float2);
+        // nM1 + 1 rows per item (LdsLayout::hext: row nM1 = row 0 for the tile folds)
+        wsp += static_cast<size_t>(L) * (nM1 + 1) * hld * sizeof(float2);
         // B holds two paths of level j1+1 or all L paths of level j1+2, whichever is larger
         size_t bcap = 2 * pslot(j1 + 1);
         if (j1 + 2 < J) bcap = std::max(bcap, static_cast<size_t>(L) * pslot(j1 + 2));
@@ -1004,6 +1005,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                                       bcap * sizeof(float2), t, Blocks{j1, J - 1, true}, j1 + 1, J - 1,
                                       smax);
         if (plan->o2_lds[j1] > static_cast<size_t>(kMaxLds)) return too_big("k_o2", j1);
+        plan->o1_lay[j1].hext = plan->o2_lay[j1].hext = 1;
     }
     plan->ws_plane = align16(wsp);
     if (plan->rb > 0)   // staged plans hold ~tens of MB per plane: bound the chunk to ~2 GB
@@ -1036,8 +1038,13 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     }
     for (int j1 = plan->rb; j1 + 1 < J && max_order >= 2; ++j1) {
         const int nM1 = g.PM >> j1, nN1 = g.PN >> j1, hld = nN1 / 2 + 1;
-        if (!export_on || plan->sq || g.PM != g.PN || plan->fam_m == 0 || plan->fam_m != plan->fam_n ||
-            plan->cap[j1] != 136)
+#ifdef WST_SQ_EXPORT   // A/B build: the SQ geometry kernels with the exported spectrum too
+        const bool sq_export = true;
+#else
+        const bool sq_export = false;
+#endif
+        if (!export_on || (plan->sq && !sq_export) || g.PM != g.PN || plan->fam_m == 0 ||
+            plan->fam_m != plan->fam_n || plan->cap[j1] != 136)
             continue;
         size_t bcap = 2 * pslot(j1 + 1);
         if (j1 + 2 < J) bcap = std::max(bcap, static_cast<size_t>(L) * pslot(j1 + 2));
@@ -1046,8 +1053,11 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
             smax = std::max(smax, static_cast<size_t>(paths_per_batch(bcap, pslot(j2), L)) * omn);
         // wide maps are written into the path arrays themselves (no S region); square: M-side
         // twiddle tables serve both dimensions
-        const size_t lds = layout(plan->o2x_lay[j1], 0, bcap * sizeof(float2), t, Blocks{j1, J - 1, false},
-                                  j1 + 1, J - 1, (g.oM > wstdev::kLpOM || g.oN > wstdev::kLpOM) ? 0 : smax);
+        const size_t lds =
+            plan->sq ? layout(plan->o2x_lay[j1], 0, bcap * sizeof(float2), t, Blocks{j1 + 1, J - 1, false}, 1, 0, smax,
+                              Blocks{j1 + 1, J - 1, false}, oms)
+                     : layout(plan->o2x_lay[j1], 0, bcap * sizeof(float2), t, Blocks{j1, J - 1, false}, j1 + 1,
+                              J - 1, (g.oM > wstdev::kLpOM || g.oN > wstdev::kLpOM) ? 0 : smax);
         // worth it when the freed spectrum lets more workgroups share a CU
         if (kMaxLds / lds <= kMaxLds / plan->o2_lds[j1]) continue;
         const int o1t = fill_cu(plan->o1_threads[j1], plan->o1_lds[j1]);
@@ -1056,6 +1066,10 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         plan->o2x_lds[j1] = lds;
         plan->o2x_threads[j1] = std::min(fill_cu(default_threads(static_cast<size_t>(nM1) * nN1), lds, 768),
                                          1024);
+#ifdef WST_SQX_THREADS
+        if (plan->sq) plan->o2x_threads[j1] = WST_SQX_THREADS;
+#endif
+        plan->o2x_lay[j1].hext = 1;
         plan->o1_lay[j1].export_full = 1;
         // one workgroup per item: splitting its batches over 2 / 4 workgroups of one XCD (as the
         // HG launches after staged levels do) measured slower here (f3 k_o2 1.57 -> 1.67 / 1.66 ms,
@@ -1206,7 +1220,7 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
     if (!do2) return WST_OK;
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
     if (plan->o2_export[j1]) {   // spectrum exported fully transformed: fold from HBM
-        plan->ops->o2(136, 0, 1, Launch{dim3(nimg * g.L * std::max(1, plan->o2x_lay[j1].nsplit)),
+        plan->ops->o2(136, plan->sq, 1, Launch{dim3(nimg * g.L * std::max(1, plan->o2x_lay[j1].nsplit)),
                                         dim3(plan->o2x_threads[j1]), plan->o2x_lds[j1], stream},
                       plan->dp, plan->o2x_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j1 + 1);
         WST_HIP_CHECK(hipGetLastError());
