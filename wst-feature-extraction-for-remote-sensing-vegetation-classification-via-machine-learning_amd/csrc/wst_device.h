@@ -1985,7 +1985,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
         // s = 2 fold fused with the rows' stage A (two-stage row sizes >= WST_FUSE_MIN)
         // N1F > 0: the spectrum's (square) size at compile time -- tile-mapped folds, reading H from
         // LDS or, in the exported-spectrum SQ kernel (HG), from HBM / L2 with the same offsets
-        constexpr int N1F = (SQ && NC > 0 && SC > 0) ? NC * SC : 0;
+        constexpr int N1F = (NC > 0 && SC > 0) ? NC * SC : 0;
         constexpr bool FUSE = N1F > 0 && SC == 2 && N1F / 2 >= WST_FUSE_MIN &&
                               wstfft::LineFFT<(N1F > 0 ? N1F / 2 : 2), true>::N2 > 1;
         const int ld2 = odd_ld(nN2);
@@ -2039,9 +2039,18 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                 if (!outd) emit(S, npath, k0, img, p.K, oM, oN, out, pooled);
             } else {
                 EpiModulus mod2{scale2, 0.f};
-                if (!(dbg & 16))
-                    lds_fft2<FM, FN, 0, MAXN, kDR, true>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
-                                                         tb.twN(j2), mod2);
+                if (!(dbg & 16)) {
+                    if constexpr (FUSE) {
+                        // stage A of the rows ran inside the fold
+                        wstfft::fft_lines_dr_stageB<(N1F > 0 ? N1F / 2 : 2), true>(
+                            B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, id);
+                        lds_fft_lines<FM, 0, MAXN, kDR, true>(B, wstfft::Lines{npath, pslot, nN2, 1, ld2}, nM2,
+                                                              tb.twM(j2), mod2);
+                    } else {
+                        lds_fft2<FM, FN, 0, MAXN, kDR, true>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
+                                                             tb.twN(j2), mod2);
+                    }
+                }
                 if (!(dbg & 64)) {
                     const int k0 = kbase + (j2 - j1 - 1) * L + l2a;
                     if (wide_lowpass(p)) {
@@ -2122,7 +2131,12 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                                 if (j1 + k < J)
                                     level(j1 + k, NN2, NN2,
                                           std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
-                                          std::integral_constant<int, 0>{}, std::integral_constant<int, NN2>{});
+#ifdef WST_HG_TILE
+                                          std::integral_constant<int, k == 1 ? 2 : 0>{},
+#else
+                                          std::integral_constant<int, 0>{},
+#endif
+                                          std::integral_constant<int, NN2>{});
                         });
                     }
                 }

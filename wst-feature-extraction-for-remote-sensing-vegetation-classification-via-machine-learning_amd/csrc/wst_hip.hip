@@ -194,6 +194,8 @@ struct wst_plan {
     std::vector<int> big_g_lds;                   // per staged level: kColModLp taps in LDS
     std::vector<int> fold_all_rows;               // per staged level: rows of the all-paths s = 2
     std::vector<size_t> fold_all_lds;             //   order-2 row pass (0: per-pair passes)
+    std::vector<size_t> o2h_lds;                  // per staged level j2: LDS of the fused s = 2
+                                                  //   order-2 path kernel k_big_o2h (0: row/col passes)
     std::vector<size_t> ws_hbig;                  // U1hat half spectra of staged j1 (per plane)
     size_t ws_tmp = 0, ws_ureal = 0, ws_part = 0, ws_csum = 0, ws_mean = 0;
     int64_t max_chunk = 2048;                     // planes per workspace chunk
@@ -873,6 +875,19 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                 }
             }
         }
+        // a whole s = 2 order-2 path per workgroup (k_big_o2h) where the half plane fits LDS: square
+        // paths of a compiled size, maps up to 8 x 8 (removes the order-2 row -> column round trip)
+        plan->o2h_lds.assign(nst, 0);
+        for (int r = 1; r < nst; ++r) {
+            const int n = g.PN >> r;
+            if (g.PM != g.PN || g.oM > 8 || g.oN > 8 || !plan->big_r[r] || plan->big_r[r]->n != n ||
+                plan->big_r[r]->o2h_threads == 0)
+                continue;
+            const size_t lds = wstbig::o2h_lds_bytes(n, noms);
+            if (lds <= static_cast<size_t>(kMaxLds)) plan->o2h_lds[r] = lds;
+        }
+        if (const char* e = diag_env("WST_O2H"))   // 0: row / column passes (A/B timing)
+            if (std::atoi(e) == 0) std::fill(plan->o2h_lds.begin(), plan->o2h_lds.end(), 0);
     } else {
         plan->prep_lds = layout(plan->prep_lay, static_cast<size_t>(g.PM) * odd_ld(g.PN) * sizeof(float2),
                                 0, t, Blocks{0, 0, true}, 0, 0, omn);
@@ -1038,11 +1053,9 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     }
     for (int j1 = plan->rb; j1 + 1 < J && max_order >= 2; ++j1) {
         const int nM1 = g.PM >> j1, nN1 = g.PN >> j1, hld = nN1 / 2 + 1;
-#ifdef WST_SQ_EXPORT   // A/B build: the SQ geometry kernels with the exported spectrum too
-        const bool sq_export = true;
-#else
-        const bool sq_export = false;
-#endif
+        // the SQ geometry kernels with the exported spectrum too (diagnostic builds: A/B timing)
+        const char* sqx_env = diag_env("WST_SQ_EXPORT");
+        const bool sq_export = sqx_env && std::atoi(sqx_env) != 0;
         if (!export_on || (plan->sq && !sq_export) || g.PM != g.PN || plan->fam_m == 0 ||
             plan->fam_m != plan->fam_n || plan->cap[j1] != 136)
             continue;
@@ -1066,9 +1079,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         plan->o2x_lds[j1] = lds;
         plan->o2x_threads[j1] = std::min(fill_cu(default_threads(static_cast<size_t>(nM1) * nN1), lds, 768),
                                          1024);
-#ifdef WST_SQX_THREADS
-        if (plan->sq) plan->o2x_threads[j1] = WST_SQX_THREADS;
-#endif
         plan->o2x_lay[j1].hext = 1;
         plan->o1_lay[j1].export_full = 1;
         // one workgroup per item: splitting its batches over 2 / 4 workgroups of one XCD (as the
@@ -1084,10 +1094,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         if (plan->o2_lds[j1] > 0) plan->o2_threads[j1] = fill_cu(plan->o2_threads[j1], plan->o2_lds[j1], 768);
     }
     if (plan->rb == 0) plan->prep_threads = fill_cu(static_cast<int>(plan->prep_threads), plan->prep_lds);
-#ifdef WST_O2T0   // A/B build: k_o2 workgroup size at the SQ 96^2 class
-    for (int j1 = plan->rb; j1 < J; ++j1)
-        if (plan->sq && plan->cap[j1] == 136 && plan->o2_lds[j1] > 0) plan->o2_threads[j1] = WST_O2T0;
-#endif
     threads_override("WST_O1_THREADS", plan->o1_threads);
     threads_override("WST_O2_THREADS", plan->o2_threads);
     threads_override("WST_O2X_THREADS", plan->o2x_threads);
@@ -1346,6 +1352,27 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         if ((rc = timer.begin(stream)) != WST_OK) return rc;
         for (int j2 = j1 + 1; j2 < plan->nst; ++j2) {
             const int m2 = PM >> j2, n2 = PN >> j2;
+            if (j2 == j1 + 1 && plan->o2h_lds[j2] > 0) {
+                // every (plane, l1, l2) path of the level in one launch, finished in the workgroup
+                O2hArgs o{};
+                o.hsrc = hbig;
+                o.psi2 = reinterpret_cast<const float*>(dp.psi2 + plan->psi2_off_host[(static_cast<size_t>(j2) * J + j1) * nq]);
+                o.pstride = 2LL * m1 * n1;
+                o.gm = gnat(j2, 0);
+                o.gn = gnat(j2, 1);
+                o.oms = noms;
+                o.j1 = j1;
+                o.j2 = j2;
+                o.L = L;
+                o.nimg = nimg;
+                o.scale = 1.f / (static_cast<float>(m1) * static_cast<float>(n1));
+                o.img0 = img0;
+                o.out = d_out;
+                o.pooled = pooled;
+                const wstlaunch::BigOps* bo = plan->big_r[j2];
+                bo->o2h(Launch{dim3(nimg * L * L), dim3(bo->o2h_threads), plan->o2h_lds[j2], stream}, dp, o);
+                continue;
+            }
             for (int l1 = 0; l1 < L; ++l1) {
                 BigArgs f = rargs(kRowFold2, j2);
                 f.hsrc = hbig;
