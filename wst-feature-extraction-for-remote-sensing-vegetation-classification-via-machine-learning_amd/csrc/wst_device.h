@@ -109,6 +109,9 @@ struct LdsLayout {
                             // b % nsplit; one item's workgroups share an XCD (its L2 holds H)
     int hgroup;             // k_o2 HG split: items per dispatch group of an XCD; within a group
                             // the slots run batch-major (one batch of hgroup items, then the next)
+    int persist;            // k_o2 (SQ, spectrum in LDS): persistent workgroups loop over the items
+                            // (gridDim.x apart); the next item's half spectrum is loaded into
+                            // registers during the last batch's transforms
     int hext;               // resident levels: an item's half spectrum in the workspace holds
                             // nM1 + 1 rows (row nM1 = row 0 for the tile folds' mirrored taps;
                             // written by an exporting k_o1, formed in LDS by k_o2 otherwise)
@@ -1079,6 +1082,14 @@ __device__ __forceinline__ Tables load_tables(const DevParams& p, const LdsLayou
 }
 
 __host__ __device__ inline int odd_ld(int n) { return n | 1; }
+// Half spectra of one (plane, theta1) in the workspace: nM1 rows of hld columns, plus row nM1 =
+// row 0 when hext (resident levels), padded to a whole 16 bytes so every item's rows start
+// 16-byte aligned (k_o2 copies them with 16-byte loads; an odd float2 count left every other item
+// on the 8-byte path)
+__host__ __device__ inline long long hspec_stride(int nM1, int hld, int hext) {
+    const long long n = static_cast<long long>(nM1 + hext) * hld;
+    return hext ? (n + 1) & ~1LL : n;
+}
 
 // Streaming (non-temporal) 8-byte load / store: the half-spectrum hand-off k_o1 -> k_o2 is
 // written and read once (~0.9 GB per 2048-plane chunk at the 96^2 level), kept from displacing
@@ -1805,7 +1816,7 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
 
     // 5. split into the two rows' half spectra (columns 0..nN1/2) and export them
     const int hld = (nN1 >> 1) + 1;
-    float2* H = hexp + static_cast<long long>(item) * (nM1 + lay.hext) * hld;
+    float2* H = hexp + item * hspec_stride(nM1, hld, lay.hext);
     if (lay.export_full) {
         // in place: packed row 2t -> half-spectrum rows 2t and 2t+1 (the odd rows of A are free),
         // then the column FFTs (rows digit-reversed -> natural); k_o2 folds the fully transformed
@@ -1904,7 +1915,8 @@ constexpr int o2_min_waves(int cap) { return cap == 48 ? 6 : cap == 24 ? 5 : 1; 
 // deeper level in one batch of all LC paths (the layout's B holds LC paths of level j1 + 2, so of
 // every level below it), so each batch shape -- paths, pairs, lines, loop bounds and divisors --
 // folds at compile time.
-template <int FM, int FN, int MAXN, int SQ, int HG, int OC, int LC = 0>
+// PS: persistent form (lay.persist; SQ kernels with a compile-time level size only).
+template <int FM, int FN, int MAXN, int SQ, int HG, int OC, int LC = 0, int PS = 0>
 __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& p,
                                           const LdsLayout& lay, int j1, int nimg, long long img0,
                                           const float2* __restrict__ hexp, float* __restrict__ out,
@@ -1934,19 +1946,17 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             item = x / nsplit;
             ksplit = x - item * nsplit;
         }
+    } else if constexpr (PS) {
+        item = blockIdx.x;
     } else {
         item = xcd_item(nimg * L);
     }
-    const int local = item / L;
-    const int l1 = item - local * L;
-    const long long img = img0 + local;
     const int PM = p.PM, PN = p.PN;
     constexpr int N1C = (SQ && !HG) ? unique_level(FM, MAXN) : 0;
+    static_assert(!PS || (N1C > 0 && !HG), "persistent k_o2: SQ kernels with a compile-time level");
     const int nM1 = N1C ? N1C : PM >> j1, nN1 = N1C ? N1C : PN >> j1;
     const int n1 = nM1 * nN1;
     const int hld = (nN1 >> 1) + 1;
-    const float2* Hg = hexp + static_cast<long long>(item) * (nM1 + lay.hext) * hld;
-    const float2* H = HG ? Hg : reinterpret_cast<const float2*>(smem);
     float2* B = reinterpret_cast<float2*>(smem + lay.off_b);
     float* S = reinterpret_cast<float*>(smem + lay.off_s);
     const Tables tb = load_tables(p, lay, smem);
@@ -1955,11 +1965,33 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     // order-2 path sizes: <= MAXN / 2 below an LDS-resident level of class MAXN, <= MAXN after a
     // big level
     constexpr int PHI = (SQ && !HG) ? MAXN / 2 : MAXN;
+    // persistent form: the next item's half spectrum (16-byte rows, hspec_stride) in KP float4
+    // registers per thread (host: nM1 hld / 2 <= KP * blockDim.x, blockDim.x >= 512)
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    constexpr int KP = PS ? (N1C * (N1C / 2 + 1) / 2 + 511) / 512 : 1;
+    f4v pf[KP];
+    const int total = nimg * L;
+    bool first = true;
+    for (;;) {   // one pass per item (the persistent form loops)
+    const int local = item / L;
+    const int l1 = item - local * L;
+    const long long img = img0 + local;
+    const int next = item + static_cast<int>(gridDim.x);
+    const float2* Hg = hexp + item * hspec_stride(nM1, hld, lay.hext);
+    const float2* H = HG ? Hg : reinterpret_cast<const float2*>(smem);
 
     if constexpr (!HG) {
         // 1. half spectrum rows -> LDS, then the column FFTs (rows digit-reversed -> natural)
         float2* Hl = reinterpret_cast<float2*>(smem);
-        if (!(dbg & 1024)) copy_to_lds(Hl, Hg, nM1 * hld);
+        if (PS && !first) {
+            f4v* d4 = reinterpret_cast<f4v*>(Hl);
+            const int n4 = (nM1 * hld) >> 1;
+#pragma unroll
+            for (int k = 0; k < KP; ++k)
+                if (threadIdx.x + k * blockDim.x < n4) d4[threadIdx.x + k * blockDim.x] = pf[k];
+        } else if (!(dbg & 1024)) {
+            copy_to_lds(Hl, Hg, nM1 * hld);
+        }
         __syncthreads();
         if (!(dbg & 4))
             lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(
@@ -2019,6 +2051,17 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                 }
             }
             __syncthreads();
+            if constexpr (PS) {
+                // the item's last fold has read the spectrum: load the next item's while this
+                // batch transforms (registers survive the barriers; stored at the next item start)
+                if (j2 == J - 1 && l2a + pb >= L && next < total) {
+                    const f4v* s4 = reinterpret_cast<const f4v*>(hexp + next * hspec_stride(nM1, hld, lay.hext));
+                    const int n4 = (nM1 * hld) >> 1;
+#pragma unroll
+                    for (int k = 0; k < KP; ++k)
+                        pf[k] = __builtin_nontemporal_load(s4 + min(static_cast<int>(threadIdx.x + k * blockDim.x), n4 - 1));
+                }
+            }
             const float scale2 = 1.f / static_cast<float>(n1);
             if constexpr (SQ) {
                 // rows, then the column pass fused with |.| and the S2 low-pass
@@ -2149,6 +2192,14 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
         for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
                   std::integral_constant<int, 0>{});
     }
+    if constexpr (!PS) {
+        break;
+    } else {
+        if (next >= total) break;
+        item = next;
+        first = false;
+    }
+    }   // item loop
 }
 
 
@@ -2161,6 +2212,12 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
         if (p.oM == 4 && p.oN == 4 && lay.oms == 4) {
             if constexpr (unique_level(FM, MAXN) > 0) {
                 if (p.L == 8) {
+                    if constexpr (!HG)
+                        if (lay.persist) {
+                            k_o2_body<FM, FN, MAXN, SQ, HG, 4, 8, 1>(smem, p, lay, j1, nimg, img0, hexp, out, pooled,
+                                                                     j2first);
+                            return;
+                        }
                     k_o2_body<FM, FN, MAXN, SQ, HG, 4, 8>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
                     return;
                 }
