@@ -156,12 +156,11 @@ def test_staged_wide_output_maps_against_oracle(M, N, J, L):
     assert_parity(got, ref, TOL, f"staged {M}x{N} J={J}")
 
 
-@pytest.mark.parametrize("M,J,L", [(224, 5, 4),     # 288^2 padded: 144^2 fused paths, 7 x 7 maps
-                                   (256, 5, 3)])    # 320^2 padded: 160^2 fused paths, 8 x 8, odd L
-def test_fused_order2_paths_against_oracle(M, J, L):
-    """The s = 2 order-2 level of a staged j1 runs one whole path per workgroup (k_big_o2h: the two
-    row-parity halves of the inverse transform, the odd one parked in registers) at every compiled
-    path size it serves besides c5's 192^2 (goldens above): 144^2 and 160^2, against the oracle."""
+@pytest.mark.parametrize("M,J,L", [(224, 5, 4),     # 288^2 padded: 144^2 staged paths, 7 x 7 maps
+                                   (256, 5, 3)])    # 320^2 padded: 160^2 staged paths, 8 x 8, odd L
+def test_staged_order2_path_sizes_against_oracle(M, J, L):
+    """Staged s = 2 order-2 levels at the compiled staged path sizes besides c5's 192^2 (goldens
+    above): 144^2 and 160^2 paths of 288^2 / 320^2 padded planes, against the oracle."""
     x = np.random.default_rng(8).integers(0, 256, (2, M, M), dtype=np.uint8).astype(np.float32) / 255
     ref = kr.Scattering2D(J=J, shape=(M, M), L=L)(x)
     got = NpS(J=J, shape=(M, M), L=L)(x)

@@ -110,8 +110,8 @@ struct LdsLayout {
     int hgroup;             // k_o2 HG split: items per dispatch group of an XCD; within a group
                             // the slots run batch-major (one batch of hgroup items, then the next)
     int persist;            // k_o2 (SQ, spectrum in LDS): persistent workgroups loop over the items
-                            // (gridDim.x apart); the next item's half spectrum is loaded into
-                            // registers during the last batch's transforms
+                            // (gridDim.x apart); 1: the next item's half spectrum is loaded into
+                            // registers during the last batch's transforms, 2: no prefetch
     int hext;               // resident levels: an item's half spectrum in the workspace holds
                             // nM1 + 1 rows (row nM1 = row 0 for the tile folds' mirrored taps;
                             // written by an exporting k_o1, formed in LDS by k_o2 otherwise)
@@ -1983,7 +1983,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     if constexpr (!HG) {
         // 1. half spectrum rows -> LDS, then the column FFTs (rows digit-reversed -> natural)
         float2* Hl = reinterpret_cast<float2*>(smem);
-        if (PS && !first) {
+        if (PS && !first && lay.persist == 1) {
             f4v* d4 = reinterpret_cast<f4v*>(Hl);
             const int n4 = (nM1 * hld) >> 1;
 #pragma unroll
@@ -2054,7 +2054,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             if constexpr (PS) {
                 // the item's last fold has read the spectrum: load the next item's while this
                 // batch transforms (registers survive the barriers; stored at the next item start)
-                if (j2 == J - 1 && l2a + pb >= L && next < total) {
+                if (j2 == J - 1 && l2a + pb >= L && next < total && lay.persist == 1) {
                     const f4v* s4 = reinterpret_cast<const f4v*>(hexp + next * hspec_stride(nM1, hld, lay.hext));
                     const int n4 = (nM1 * hld) >> 1;
 #pragma unroll

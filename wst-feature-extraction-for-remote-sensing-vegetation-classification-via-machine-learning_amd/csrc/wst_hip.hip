@@ -195,8 +195,6 @@ struct wst_plan {
     std::vector<int> big_g_lds;                   // per staged level: kColModLp taps in LDS
     std::vector<int> fold_all_rows;               // per staged level: rows of the all-paths s = 2
     std::vector<size_t> fold_all_lds;             //   order-2 row pass (0: per-pair passes)
-    std::vector<size_t> o2h_lds;                  // per staged level j2: LDS of the fused s = 2
-                                                  //   order-2 path kernel k_big_o2h (0: row/col passes)
     std::vector<size_t> ws_hbig;                  // U1hat half spectra of staged j1 (per plane)
     size_t ws_tmp = 0, ws_ureal = 0, ws_part = 0, ws_csum = 0, ws_mean = 0;
     int64_t max_chunk = 2048;                     // planes per workspace chunk
@@ -876,19 +874,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                 }
             }
         }
-        // a whole s = 2 order-2 path per workgroup (k_big_o2h) where the half plane fits LDS: square
-        // paths of a compiled size, maps up to 8 x 8 (removes the order-2 row -> column round trip)
-        plan->o2h_lds.assign(nst, 0);
-        for (int r = 1; r < nst; ++r) {
-            const int n = g.PN >> r;
-            if (g.PM != g.PN || g.oM > 8 || g.oN > 8 || !plan->big_r[r] || plan->big_r[r]->n != n ||
-                plan->big_r[r]->o2h_threads == 0)
-                continue;
-            const size_t lds = wstbig::o2h_lds_bytes(n, noms);
-            if (lds <= static_cast<size_t>(kMaxLds)) plan->o2h_lds[r] = lds;
-        }
-        if (const char* e = diag_env("WST_O2H"))   // 0: row / column passes (A/B timing)
-            if (std::atoi(e) == 0) std::fill(plan->o2h_lds.begin(), plan->o2h_lds.end(), 0);
     } else {
         plan->prep_lds = layout(plan->prep_lay, static_cast<size_t>(g.PM) * odd_ld(g.PN) * sizeof(float2),
                                 0, t, Blocks{0, 0, true}, 0, 0, omn);
@@ -1113,8 +1098,9 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     {
         int ncu = 0;
         WST_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, plan->device));
-        bool persist = false;
-        if (const char* e = diag_env("WST_O2_PERSIST")) persist = std::atoi(e) != 0;
+        int persist = 0, grid_mult = 0;   // diagnostic builds: 1 prefetching, 2 plain; grid multiple
+        if (const char* e = diag_env("WST_O2_PERSIST")) persist = std::atoi(e);
+        if (const char* e = diag_env("WST_O2_GRID")) grid_mult = std::atoi(e);
         for (int j1 = plan->rb; j1 + 1 < J && max_order >= 2; ++j1) {
             plan->o2_grid[j1] = 0;
             const int nM1 = g.PM >> j1, hld = (g.PN >> j1) / 2 + 1;
@@ -1126,8 +1112,8 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
             if (!persist || !form) continue;
             const int per_cu = std::max<int>(1, std::min<int>(kMaxLds / static_cast<int>(plan->o2_lds[j1]),
                                                                2048 / plan->o2_threads[j1]));
-            plan->o2_lay[j1].persist = 1;
-            plan->o2_grid[j1] = ncu * per_cu;
+            plan->o2_lay[j1].persist = persist;
+            plan->o2_grid[j1] = ncu * (grid_mult > 0 ? grid_mult : per_cu);
         }
     }
     WST_HIP_CHECK(plan->ops->set_attrs());
@@ -1377,27 +1363,6 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         if ((rc = timer.begin(stream)) != WST_OK) return rc;
         for (int j2 = j1 + 1; j2 < plan->nst; ++j2) {
             const int m2 = PM >> j2, n2 = PN >> j2;
-            if (j2 == j1 + 1 && plan->o2h_lds[j2] > 0) {
-                // every (plane, l1, l2) path of the level in one launch, finished in the workgroup
-                O2hArgs o{};
-                o.hsrc = hbig;
-                o.psi2 = reinterpret_cast<const float*>(dp.psi2 + plan->psi2_off_host[(static_cast<size_t>(j2) * J + j1) * nq]);
-                o.pstride = 2LL * m1 * n1;
-                o.gm = gnat(j2, 0);
-                o.gn = gnat(j2, 1);
-                o.oms = noms;
-                o.j1 = j1;
-                o.j2 = j2;
-                o.L = L;
-                o.nimg = nimg;
-                o.scale = 1.f / (static_cast<float>(m1) * static_cast<float>(n1));
-                o.img0 = img0;
-                o.out = d_out;
-                o.pooled = pooled;
-                const wstlaunch::BigOps* bo = plan->big_r[j2];
-                bo->o2h(Launch{dim3(nimg * L * L), dim3(bo->o2h_threads), plan->o2h_lds[j2], stream}, dp, o);
-                continue;
-            }
             for (int l1 = 0; l1 < L; ++l1) {
                 BigArgs f = rargs(kRowFold2, j2);
                 f.hsrc = hbig;

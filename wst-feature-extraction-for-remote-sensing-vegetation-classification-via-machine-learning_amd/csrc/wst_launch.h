@@ -40,9 +40,6 @@ struct BigOps {
     hipError_t (*set_attrs)();
     void (*rows)(bool inverse, const Launch&, const DevParams&, const wstbig::BigArgs&);
     void (*cols)(bool inverse, const Launch&, const DevParams&, const wstbig::BigArgs&);
-    // fused s = 2 order-2 path kernel (k_big_o2h) for square N x N paths: workgroup size, 0 = none
-    int o2h_threads;
-    void (*o2h)(const Launch&, const DevParams&, const wstbig::O2hArgs&);
 };
 // Compiled line lengths; every other length runs the N = 0 instantiation (generic DFT, n at run
 // time).  Keep in step with the Makefile's BIGNS.

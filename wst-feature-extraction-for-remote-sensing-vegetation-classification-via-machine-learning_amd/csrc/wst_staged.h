@@ -454,162 +454,6 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
     }
 }
 
-// --------------------------------------------------------------------------------------------
-// k_big_o2h: one whole s = 2 order-2 path of a staged level per workgroup (square N x N path of a
-// 2N x 2N level j1), so the path never makes the row -> column round trip through HBM.
-//   Y = fold_2(U1hat * psi_{j2, l2})                        (N x N, from the Hermitian half spectra)
-//   y = ifft2(Y), split by the parity r of the row frequency:  Y_r[k'][l] = Y[2k' + r][l] (N/2 x N),
-//       Z_r = ifft2_{N/2 x N}(Y_r),  y[m' + h N/2][n] = Z_0[m'][n] + (-1)^h e^{+2 pi i m'/N} Z_1[m'][n]
-//   Z_1 is formed first in LDS and parked in registers (N/2 / kHalfG values per thread), Z_0 then
-//   takes the same LDS; |y| * scale and the phi low-pass at the kept points
-//       S[a][c] = sum_q GN[q][c] sum_p GM[p][a] |y[p][q]|
-//   (the same natural tap matrices as kColModLp + k_big_final) finish in registers, and the map is
-//   emitted like every other kernel's.  Threads: kHalfG per column q (thread t: q = t % N, rows
-//   m' = t / N + kHalfG i), so a thread's partial low-pass sums share one column.
-// Replaces kRowFold2 + kColModLp + k_big_final (kind 2) for the first order-2 level of a staged j1
-// (kymatio's cdgmm -> subsample_fourier(k = 2) -> ifft2 -> modulus ->
-// phi low-pass of order 2; reference call sites train_and_save_model.py:359-376).
-// --------------------------------------------------------------------------------------------
-constexpr int kHalfG = 4;
-// path sizes the fused kernel serves: N/2 rows split over kHalfG thread groups, <= 1024 threads
-template <int N>
-constexpr bool o2h_size_ok() {
-    return N >= 16 && N % (2 * kHalfG) == 0 && kHalfG * N <= 1024 && (kHalfG * N) % 64 == 0 &&
-           (N / 2) <= wstfft::kMaxFamilyN;
-}
-// LDS bytes: half plane | row twiddles (N) | column twiddles (N/2) | GM (N x oms) | wave partials | S
-inline size_t o2h_lds_bytes(int n, int oms) {
-    const size_t h = static_cast<size_t>(n) / 2, ld = static_cast<size_t>(n | 1);
-    const size_t waves = (static_cast<size_t>(kHalfG) * n + 63) / 64;
-    return h * ld * 8 + static_cast<size_t>(n) * 8 + h * 8 + static_cast<size_t>(n) * oms * 4 +
-           waves * 64 * 4 + 64 * 4;
-}
-
-struct O2hArgs {
-    const float2* hsrc;   // half spectra of level j1: 2N rows x (N + 1) columns per (plane, l1)
-    const float* psi2;    // filters of (j2, j1) as floats: pair q's bin b at [q pstride + 2 b + (l2 & 1)]
-    long long pstride;    // floats between filter pairs
-    const float* gm;      // natural-order tap matrices of level j2: GM (N x oms), GN (N x oms)
-    const float* gn;
-    int oms, j1, j2, L, nimg;
-    float scale;          // 1 / (2N)^2 (subsample_fourier's mean over the aliases and ifft2's 1/N^2)
-    long long img0;
-    float* out;
-    int pooled;
-};
-
-template <int N>
-__global__ void __launch_bounds__(N > 0 ? kHalfG * N : 64) k_big_o2h(DevParams p, O2hArgs a) {
-    constexpr int T = kHalfG * N, H = N / 2, LD = N | 1, NR = H / kHalfG, N1 = 2 * N, HLD = N + 1;
-    constexpr int NW = (T + 63) / 64;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float2* A = reinterpret_cast<float2*>(smem);
-    float2* twR = A + H * LD;
-    float2* twC = twR + N;
-    float* gm = reinterpret_cast<float*>(twC + H);
-    const int oms = a.oms, oM = p.oM, oN = p.oN;
-    float* red = gm + N * oms;
-    float* S = red + NW * 64;
-    const int tid = threadIdx.x;
-    // path index: consecutive dispatch slots of one XCD take consecutive paths, so the L paths of
-    // an item (plane, l1) fold from one spectrum through that XCD's L2
-    const int total = a.nimg * a.L * a.L;
-    int w = blockIdx.x;
-    if ((total & 7) == 0) w = (blockIdx.x & 7) * (total >> 3) + (blockIdx.x >> 3);
-    const int item = w / a.L, l2 = w - item * a.L;
-    const int plane = item / a.L, l1 = item - plane * a.L;
-    {
-        const float2* gr = level_tw(p, a.j2, 1);       // n = N
-        const float2* gc = level_tw(p, a.j2 + 1, 0);   // n = N / 2
-        for (int i = tid; i < N; i += T) twR[i] = gr[i];
-        for (int i = tid; i < H; i += T) twC[i] = gc[i];
-        for (int i = tid; i < N * oms; i += T) gm[i] = a.gm[i];
-    }
-    const int q = tid % N, g = tid / N;
-    float gnq[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) gnq[c] = c < oN ? a.gn[q * oms + c] : 0.f;
-    const float2* Hs = a.hsrc + static_cast<long long>(item) * N1 * HLD;
-    const float* fp = a.psi2 + (l2 >> 1) * a.pstride + (l2 & 1);
-    wstfft::EpiIdentity id;
-    float2 z1[NR];
-    // rows of parity r: fold, row and column transforms in LDS (r = 1 first, parked in registers)
-#pragma unroll 1
-    for (int r = 1; r >= 0; --r) {
-#pragma unroll 4
-        for (int i = 0; i < NR; ++i) {
-            const int kp = g + kHalfG * i;
-            const int k = 2 * kp + r;
-            float2 acc = make_float2(0.f, 0.f);
-#pragma unroll
-            for (int al = 0; al < 2; ++al) {
-                const int kr = k + al * N;
-                const int krm = kr == 0 ? 0 : N1 - kr;
-                const float2 h0 = Hs[kr * HLD + q];
-                float2 h1;
-                if (q == 0) {
-                    h1 = Hs[kr * HLD + N];
-                } else {
-                    h1 = Hs[krm * HLD + (N - q)];
-                    h1.y = -h1.y;
-                }
-                const float f0 = fp[2 * (kr * N1 + q)], f1 = fp[2 * (kr * N1 + q + N)];
-                acc.x = fmaf(h0.x, f0, fmaf(h1.x, f1, acc.x));
-                acc.y = fmaf(h0.y, f0, fmaf(h1.y, f1, acc.y));
-            }
-            A[kp * LD + q] = acc;
-        }
-        __syncthreads();
-        wstfft::fft_lines<N, true>(A, wstfft::Lines(1, 0, H, LD, 1), twR, id);
-        wstfft::fft_lines<H, true>(A, wstfft::Lines(1, 0, N, 1, LD), twC, id);
-        if (r == 1) {
-#pragma unroll
-            for (int i = 0; i < NR; ++i) z1[i] = A[(g + kHalfG * i) * LD + q];
-            __syncthreads();
-        }
-    }
-    // y rows m' and m' + N/2 of column q: modulus, then the GM contraction of the thread's rows
-    float V[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) V[c] = 0.f;
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-        const int kp = g + kHalfG * i;
-        const float2 z0 = A[kp * LD + q];
-        const float2 wv = twR[kp];   // e^{-2 pi i m'/N}: the inverse twiddle is its conjugate
-        const float tx = fmaf(wv.x, z1[i].x, wv.y * z1[i].y);
-        const float ty = fmaf(wv.x, z1[i].y, -wv.y * z1[i].x);
-        const float m0 = __builtin_amdgcn_sqrtf(fmaf(z0.x + tx, z0.x + tx, (z0.y + ty) * (z0.y + ty))) * a.scale;
-        const float m1 = __builtin_amdgcn_sqrtf(fmaf(z0.x - tx, z0.x - tx, (z0.y - ty) * (z0.y - ty))) * a.scale;
-        const float* g0 = gm + kp * oms;
-        const float* g1 = gm + (kp + H) * oms;
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-            if (c < oM) V[c] = fmaf(g0[c], m0, fmaf(g1[c], m1, V[c]));
-    }
-    // S[a][c] = sum over threads of V[a] GN[q][c]: wave sums, then the waves' partials
-    const int lane = tid & 63, wv = tid >> 6;
-#pragma unroll
-    for (int ra = 0; ra < 8; ++ra) {
-        if (ra >= oM) break;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            if (c >= oN) break;
-            const float s = wstdev::group_sum<64>(V[ra] * gnq[c]);
-            if (lane == 0) red[wv * 64 + ra * oN + c] = s;
-        }
-    }
-    __syncthreads();
-    if (tid < oM * oN) {
-        float s = 0.f;
-        for (int k = 0; k < NW; ++k) s += red[k * 64 + tid];
-        S[tid] = s;
-    }
-    __syncthreads();
-    const int kk = p.o2_base[a.j1 * a.L + l1] + (a.j2 - a.j1 - 1) * a.L + l2;
-    wstdev::emit(S, 1, kk, a.img0 + plane, p.K, oM, oN, a.out, a.pooled);
-}
-
 // Size-independent kernels: defined in one object only (wst_staged.hip with WST_BIG_N = 0).
 #ifdef WST_BIG_COMMON_KERNELS
 // --------------------------------------------------------------------------------------------

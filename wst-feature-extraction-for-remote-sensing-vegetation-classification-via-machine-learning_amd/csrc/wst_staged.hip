@@ -27,10 +27,6 @@ hipError_t set_attrs() {
         if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      wstdev::kMaxLds)) != hipSuccess)
             return e;
-    if constexpr (wstbig::o2h_size_ok<N>())
-        if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(wstbig::k_big_o2h<N>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, wstdev::kMaxLds)) != hipSuccess)
-            return e;
     return hipSuccess;
 }
 
@@ -48,18 +44,12 @@ void cols(bool inverse, const Launch& q, const DevParams& dp, const wstbig::BigA
         hipLaunchKernelGGL((wstbig::k_big_cols<N, false>), q.grid, q.block, q.lds, q.st, dp, a);
 }
 
-void o2h(const Launch& q, const DevParams& dp, const wstbig::O2hArgs& a) {
-    if constexpr (wstbig::o2h_size_ok<N>())
-        hipLaunchKernelGGL((wstbig::k_big_o2h<N>), q.grid, q.block, q.lds, q.st, dp, a);
-}
-
 }  // namespace
 
 #define WST_BIG_NAME(N_) WST_BIG_GETTER(N_)
 #define WST_BIG_EXPAND(N_) WST_BIG_NAME(N_)
 const BigOps& WST_BIG_EXPAND(WST_BIG_N)() {
-    static const BigOps ops{N, set_attrs, rows, cols,
-                            wstbig::o2h_size_ok<N>() ? wstbig::kHalfG * N : 0, o2h};
+    static const BigOps ops{N, set_attrs, rows, cols};
     return ops;
 }
 
