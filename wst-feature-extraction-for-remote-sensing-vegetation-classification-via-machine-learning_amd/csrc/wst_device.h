@@ -36,17 +36,13 @@
 #define WST_DBG_MASK(p) 0
 #endif
 
-#ifndef WST_FUSE_MIN
-#define WST_FUSE_MIN 48
-#endif
-#ifndef WST_FUSE1_MIN
-#define WST_FUSE1_MIN 48
-#endif
-#ifndef WST_FUSE_GRP
-#define WST_FUSE_GRP 4
-#endif
-
 namespace wstdev {
+
+// s = 2 order-2 fold / order-1 product fused with the rows' stage A from these row lengths on
+// (compile-time square levels); elements whose fold loads one fused unit keeps in flight
+constexpr int kFuseMin = 48;
+constexpr int kFuse1Min = 48;
+constexpr int kFuseGroup = 4;
 
 constexpr int kMaxLds = 160 * 1024;
 constexpr int kMaxO = 8;  // outputs per thread per generic-DFT chunk
@@ -109,9 +105,6 @@ struct LdsLayout {
                             // b % nsplit; one item's workgroups share an XCD (its L2 holds H)
     int hgroup;             // k_o2 HG split: items per dispatch group of an XCD; within a group
                             // the slots run batch-major (one batch of hgroup items, then the next)
-    int persist;            // k_o2 (SQ, spectrum in LDS): persistent workgroups loop over the items
-                            // (gridDim.x apart); 1: the next item's half spectrum is loaded into
-                            // registers during the last batch's transforms, 2: no prefetch
     int hext;               // resident levels: an item's half spectrum in the workspace holds
                             // nM1 + 1 rows (row nM1 = row 0 for the tile folds' mirrored taps;
                             // written by an exporting k_o1, formed in LDS by k_o2 otherwise)
@@ -1522,8 +1515,8 @@ __device__ __forceinline__ void fold2_s2_rowA(const float2* __restrict__ H, cons
             // pin both paths' sums here: sunk to their DFTs, the other path's filter values stayed
             // live (spilled) across the first path's transform
             asm volatile("" : "+v"(x0[e].x), "+v"(x0[e].y), "+v"(x1[e].x), "+v"(x1[e].y));
-            // at most WST_FUSE_GRP elements' loads in flight (register budget of 4 waves per SIMD)
-            if constexpr ((e + 1) % WST_FUSE_GRP == 0) __builtin_amdgcn_sched_barrier(0);
+            // at most kFuseGroup elements' loads in flight (register budget of 4 waves per SIMD)
+            if constexpr ((e + 1) % kFuseGroup == 0) __builtin_amdgcn_sched_barrier(0);
         });
         wstfft::rfft<NA, true>(x0);
         wstfft::rfft<NA, true>(x1);
@@ -1758,7 +1751,7 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     // stage A (fold1_rowA)
     // (SQ geometry kernels: c2 k_o1 j1 = 0 0.778 -> 0.726 ms; the non-SQ 136^2 level of f3 measured
     // 0.78 -> 0.79, so the exported-spectrum kernels keep the separate fold)
-    constexpr bool FUSE1 = SQ && N1C >= WST_FUSE1_MIN && wstfft::LineFFT<(N1C > 0 ? N1C : 2), true>::N2 > 1;
+    constexpr bool FUSE1 = SQ && N1C >= kFuse1Min && wstfft::LineFFT<(N1C > 0 ? N1C : 2), true>::N2 > 1;
     const bool fused1 = FUSE1 && j1 == 0;
     EpiModulus mod1{1.f / (static_cast<float>(PM) * static_cast<float>(PN)), 0.f};
     if (fused1) {
@@ -1915,8 +1908,7 @@ constexpr int o2_min_waves(int cap) { return cap == 48 ? 6 : cap == 24 ? 5 : 1; 
 // deeper level in one batch of all LC paths (the layout's B holds LC paths of level j1 + 2, so of
 // every level below it), so each batch shape -- paths, pairs, lines, loop bounds and divisors --
 // folds at compile time.
-// PS: persistent form (lay.persist; SQ kernels with a compile-time level size only).
-template <int FM, int FN, int MAXN, int SQ, int HG, int OC, int LC = 0, int PS = 0>
+template <int FM, int FN, int MAXN, int SQ, int HG, int OC, int LC = 0>
 __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& p,
                                           const LdsLayout& lay, int j1, int nimg, long long img0,
                                           const float2* __restrict__ hexp, float* __restrict__ out,
@@ -1946,14 +1938,11 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             item = x / nsplit;
             ksplit = x - item * nsplit;
         }
-    } else if constexpr (PS) {
-        item = blockIdx.x;
     } else {
         item = xcd_item(nimg * L);
     }
     const int PM = p.PM, PN = p.PN;
     constexpr int N1C = (SQ && !HG) ? unique_level(FM, MAXN) : 0;
-    static_assert(!PS || (N1C > 0 && !HG), "persistent k_o2: SQ kernels with a compile-time level");
     const int nM1 = N1C ? N1C : PM >> j1, nN1 = N1C ? N1C : PN >> j1;
     const int n1 = nM1 * nN1;
     const int hld = (nN1 >> 1) + 1;
@@ -1965,33 +1954,16 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     // order-2 path sizes: <= MAXN / 2 below an LDS-resident level of class MAXN, <= MAXN after a
     // big level
     constexpr int PHI = (SQ && !HG) ? MAXN / 2 : MAXN;
-    // persistent form: the next item's half spectrum (16-byte rows, hspec_stride) in KP float4
-    // registers per thread (host: nM1 hld / 2 <= KP * blockDim.x, blockDim.x >= 512)
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    constexpr int KP = PS ? (N1C * (N1C / 2 + 1) / 2 + 511) / 512 : 1;
-    f4v pf[KP];
-    const int total = nimg * L;
-    bool first = true;
-    for (;;) {   // one pass per item (the persistent form loops)
     const int local = item / L;
     const int l1 = item - local * L;
     const long long img = img0 + local;
-    const int next = item + static_cast<int>(gridDim.x);
     const float2* Hg = hexp + item * hspec_stride(nM1, hld, lay.hext);
     const float2* H = HG ? Hg : reinterpret_cast<const float2*>(smem);
 
     if constexpr (!HG) {
         // 1. half spectrum rows -> LDS, then the column FFTs (rows digit-reversed -> natural)
         float2* Hl = reinterpret_cast<float2*>(smem);
-        if (PS && !first && lay.persist == 1) {
-            f4v* d4 = reinterpret_cast<f4v*>(Hl);
-            const int n4 = (nM1 * hld) >> 1;
-#pragma unroll
-            for (int k = 0; k < KP; ++k)
-                if (threadIdx.x + k * blockDim.x < n4) d4[threadIdx.x + k * blockDim.x] = pf[k];
-        } else if (!(dbg & 1024)) {
-            copy_to_lds(Hl, Hg, nM1 * hld);
-        }
+        if (!(dbg & 1024)) copy_to_lds(Hl, Hg, nM1 * hld);
         __syncthreads();
         if (!(dbg & 4))
             lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(
@@ -2014,11 +1986,11 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
         constexpr int PB = decltype(pbc)::value;
         constexpr int SC = decltype(scc)::value;
         constexpr int NC = decltype(ncc)::value;
-        // s = 2 fold fused with the rows' stage A (two-stage row sizes >= WST_FUSE_MIN)
+        // s = 2 fold fused with the rows' stage A (two-stage row sizes >= kFuseMin)
         // N1F > 0: the spectrum's (square) size at compile time -- tile-mapped folds, reading H from
         // LDS or, in the exported-spectrum SQ kernel (HG), from HBM / L2 with the same offsets
-        constexpr int N1F = (NC > 0 && SC > 0) ? NC * SC : 0;
-        constexpr bool FUSE = N1F > 0 && SC == 2 && N1F / 2 >= WST_FUSE_MIN &&
+        constexpr int N1F = (SQ && NC > 0 && SC > 0) ? NC * SC : 0;
+        constexpr bool FUSE = N1F > 0 && SC == 2 && N1F / 2 >= kFuseMin &&
                               wstfft::LineFFT<(N1F > 0 ? N1F / 2 : 2), true>::N2 > 1;
         const int ld2 = odd_ld(nN2);
         const int pslot = nM2 * ld2;
@@ -2051,17 +2023,6 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                 }
             }
             __syncthreads();
-            if constexpr (PS) {
-                // the item's last fold has read the spectrum: load the next item's while this
-                // batch transforms (registers survive the barriers; stored at the next item start)
-                if (j2 == J - 1 && l2a + pb >= L && next < total && lay.persist == 1) {
-                    const f4v* s4 = reinterpret_cast<const f4v*>(hexp + next * hspec_stride(nM1, hld, lay.hext));
-                    const int n4 = (nM1 * hld) >> 1;
-#pragma unroll
-                    for (int k = 0; k < KP; ++k)
-                        pf[k] = __builtin_nontemporal_load(s4 + min(static_cast<int>(threadIdx.x + k * blockDim.x), n4 - 1));
-                }
-            }
             const float scale2 = 1.f / static_cast<float>(n1);
             if constexpr (SQ) {
                 // rows, then the column pass fused with |.| and the S2 low-pass
@@ -2082,18 +2043,9 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                 if (!outd) emit(S, npath, k0, img, p.K, oM, oN, out, pooled);
             } else {
                 EpiModulus mod2{scale2, 0.f};
-                if (!(dbg & 16)) {
-                    if constexpr (FUSE) {
-                        // stage A of the rows ran inside the fold
-                        wstfft::fft_lines_dr_stageB<(N1F > 0 ? N1F / 2 : 2), true>(
-                            B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, id);
-                        lds_fft_lines<FM, 0, MAXN, kDR, true>(B, wstfft::Lines{npath, pslot, nN2, 1, ld2}, nM2,
-                                                              tb.twM(j2), mod2);
-                    } else {
-                        lds_fft2<FM, FN, 0, MAXN, kDR, true>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
-                                                             tb.twN(j2), mod2);
-                    }
-                }
+                if (!(dbg & 16))
+                    lds_fft2<FM, FN, 0, MAXN, kDR, true>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
+                                                         tb.twN(j2), mod2);
                 if (!(dbg & 64)) {
                     const int k0 = kbase + (j2 - j1 - 1) * L + l2a;
                     if (wide_lowpass(p)) {
@@ -2174,12 +2126,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                                 if (j1 + k < J)
                                     level(j1 + k, NN2, NN2,
                                           std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
-#ifdef WST_HG_TILE
-                                          std::integral_constant<int, k == 1 ? 2 : 0>{},
-#else
-                                          std::integral_constant<int, 0>{},
-#endif
-                                          std::integral_constant<int, NN2>{});
+                                          std::integral_constant<int, 0>{}, std::integral_constant<int, NN2>{});
                         });
                     }
                 }
@@ -2192,14 +2139,6 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
         for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
                   std::integral_constant<int, 0>{});
     }
-    if constexpr (!PS) {
-        break;
-    } else {
-        if (next >= total) break;
-        item = next;
-        first = false;
-    }
-    }   // item loop
 }
 
 
@@ -2212,12 +2151,6 @@ __global__ void __launch_bounds__(1024, o2_min_waves(MAXN)) k_o2(DevParams p, Ld
         if (p.oM == 4 && p.oN == 4 && lay.oms == 4) {
             if constexpr (unique_level(FM, MAXN) > 0) {
                 if (p.L == 8) {
-                    if constexpr (!HG)
-                        if (lay.persist) {
-                            k_o2_body<FM, FN, MAXN, SQ, HG, 4, 8, 1>(smem, p, lay, j1, nimg, img0, hexp, out, pooled,
-                                                                     j2first);
-                            return;
-                        }
                     k_o2_body<FM, FN, MAXN, SQ, HG, 4, 8>(smem, p, lay, j1, nimg, img0, hexp, out, pooled, j2first);
                     return;
                 }

@@ -170,7 +170,6 @@ struct wst_plan {
     LdsLayout prep_lay{};
     std::vector<int> o1_threads, o2_threads, cap;
     std::vector<size_t> o1_lds, o2_lds;
-    std::vector<int> o2_grid;                     // persistent k_o2: workgroups per launch (0: one per item)
     std::vector<LdsLayout> o1_lay, o2_lay;
     // HBM-staged leading levels (n > kBigMinN): wst_staged.h
     int rb = 0;
@@ -889,7 +888,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     plan->o2_lds.assign(J, 0);
     plan->o1_lay.assign(J, LdsLayout{});
     plan->o2_lay.assign(J, LdsLayout{});
-    plan->o2_grid.assign(J, 0);
     plan->ws_h_off.assign(J, 0);
     plan->ws_xhat = static_cast<size_t>(g.PM) * g.PN * sizeof(float2);
     size_t wsp = plan->ws_xhat;
@@ -1093,29 +1091,6 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
             return fail(WST_ERR_INVALID, "k_o1 at level " + std::to_string(j1) + ": " +
                                              std::to_string(plan->o1_threads[j1]) +
                                              " threads cannot hold the exported half spectrum (8 items each)");
-    // persistent SQ k_o2 (LdsLayout::persist): the geometries whose kernel body takes the
-    // compile-time 4 x 4, L = 8 form (wst_device.h k_o2), grid = the workgroups the CUs hold
-    {
-        int ncu = 0;
-        WST_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, plan->device));
-        int persist = 0, grid_mult = 0;   // diagnostic builds: 1 prefetching, 2 plain; grid multiple
-        if (const char* e = diag_env("WST_O2_PERSIST")) persist = std::atoi(e);
-        if (const char* e = diag_env("WST_O2_GRID")) grid_mult = std::atoi(e);
-        for (int j1 = plan->rb; j1 + 1 < J && max_order >= 2; ++j1) {
-            plan->o2_grid[j1] = 0;
-            const int nM1 = g.PM >> j1, hld = (g.PN >> j1) / 2 + 1;
-            const bool form = plan->sq && plan->cap[j1] == 136 && g.PM == g.PN && plan->fam_m == plan->fam_n &&
-                              wstdev::unique_level(plan->fam_m, 136) == nM1 && g.oM == 4 && g.oN == 4 &&
-                              plan->o2_lay[j1].oms == 4 && L == 8 && plan->o2_lay[j1].hext == 1 &&
-                              !plan->o2_export[j1] && (nM1 * hld) % 2 == 0 && plan->o2_threads[j1] >= 512 &&
-                              (nM1 * hld) / 2 <= ((nM1 * (nM1 / 2 + 1) / 2 + 511) / 512) * plan->o2_threads[j1];
-            if (!persist || !form) continue;
-            const int per_cu = std::max<int>(1, std::min<int>(kMaxLds / static_cast<int>(plan->o2_lds[j1]),
-                                                               2048 / plan->o2_threads[j1]));
-            plan->o2_lay[j1].persist = persist;
-            plan->o2_grid[j1] = ncu * (grid_mult > 0 ? grid_mult : per_cu);
-        }
-    }
     WST_HIP_CHECK(plan->ops->set_attrs());
     if (plan->rb > 0) {
         WST_HIP_CHECK(wstlaunch::wst_big_common_ops().set_attrs());
@@ -1242,9 +1217,8 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
         WST_HIP_CHECK(hipGetLastError());
         return timer.end(stream, 1 + g.J + j1);
     }
-    const int o2_wgs = plan->o2_grid[j1] > 0 ? std::min(plan->o2_grid[j1], nimg * g.L) : nimg * g.L;
     plan->ops->o2(plan->cap[j1], plan->sq, 0,
-                  Launch{dim3(o2_wgs), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
+                  Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
                   plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j1 + 1);
     WST_HIP_CHECK(hipGetLastError());
     return timer.end(stream, 1 + g.J + j1);
