@@ -206,9 +206,6 @@ WST_HD void rfft(float2 (&x)[R]) {
 // four-step line transforms
 // ---------------------------------------------------------------------------------------------
 constexpr int split_n2(int n) {  // N2 = largest divisor <= sqrt(n); 1 means a single stage
-#ifdef WST_SPLIT12_4   // A/B experiment (temporary)
-    if (n == 12) return 4;
-#endif
     if (n <= 16 || is_prime(n)) return 1;
     int best = 1;
     for (int d = 2; d * d <= n; ++d)
