@@ -43,6 +43,9 @@ namespace wstdev {
 constexpr int kFuseMin = 48;
 constexpr int kFuse1Min = 48;
 constexpr int kFuseGroup = 4;
+// SQ k_o2 of size classes up to this cap: B holds all L paths of the first order-2 level too (host:
+// bcap), so that level runs as one batch instead of L / 2 filter-pair batches
+constexpr int kWholeFirstCap = 48;
 
 constexpr int kMaxLds = 160 * 1024;
 constexpr int kMaxO = 8;  // outputs per thread per generic-DFT chunk
@@ -2078,7 +2081,8 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             constexpr int NN2 = N1C >> k;
             if constexpr ((NN2 << k) == N1C && NN2 >= 1)
                 if (j1 + k < J && j1 + k >= j2first)
-                    level(j1 + k, NN2, NN2, std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
+                    level(j1 + k, NN2, NN2,
+                          std::integral_constant<int, LC == 0 ? 0 : (k == 1 && MAXN > kWholeFirstCap) ? 2 : LC>{},
                           std::integral_constant<int, (1 << k)>{}, std::integral_constant<int, NN2>{});
         });
     } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {

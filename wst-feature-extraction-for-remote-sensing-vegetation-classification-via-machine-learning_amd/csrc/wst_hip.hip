@@ -989,9 +989,12 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
         plan->ws_h_off[j1] = wsp;
         // nM1 + 1 rows per item (LdsLayout::hext: row nM1 = row 0 for the tile folds)
         wsp += static_cast<size_t>(L) * wstdev::hspec_stride(nM1, hld, 1) * sizeof(float2);
-        // B holds two paths of level j1+1 or all L paths of level j1+2, whichever is larger
+        // B holds two paths of level j1+1 or all L paths of level j1+2, whichever is larger; the
+        // small SQ classes hold all L paths of level j1+1 (one batch: wstdev::kWholeFirstCap)
         size_t bcap = 2 * pslot(j1 + 1);
         if (j1 + 2 < J) bcap = std::max(bcap, static_cast<size_t>(L) * pslot(j1 + 2));
+        if (plan->sq && plan->cap[j1] <= wstdev::kWholeFirstCap)
+            bcap = std::max(bcap, static_cast<size_t>(L) * pslot(j1 + 1));
         size_t smax = 0;
         for (int j2 = j1 + 1; j2 < J; ++j2)
             smax = std::max(smax, static_cast<size_t>(paths_per_batch(bcap, pslot(j2), L)) * omn);
