@@ -380,15 +380,28 @@ struct LineFFT {
             p[e * g.es] = epi(v[e]);
         });
     }
-    // G = stageBp_unit then stageAp_unit: digit-reversed in -> natural out.
-    static WST_HD void stageBp_unit(float2* base, const Lines& g, const float2* tw, int u) {
+    // G = stageBp_unit then stageAp_unit: digit-reversed in -> natural out.  GL: the stage reads its
+    // inputs from `gsrc` (global memory laid out like base) instead of base.
+    template <bool GL = false>
+    static WST_HD void stageBp_unit(float2* base, const Lines& g, const float2* tw, int u,
+                                    const float2* gsrc = nullptr) {
         int k1;
         const int line = g.split(u, k1);
-        float2* p = base + g.offset(line) + (N2 * k1) * g.es;
+        const int off = g.offset(line) + (N2 * k1) * g.es;
+        float2* p = base + off;
         float2 v[N2];
         static_for<0, N2>([&](auto ec) {
             constexpr int e = decltype(ec)::value;
-            v[e] = p[e * g.es];
+            if constexpr (GL) {
+#if defined(__HIP_DEVICE_COMPILE__)
+                v[e] = __builtin_bit_cast(float2, __builtin_nontemporal_load(
+                                                      reinterpret_cast<const unsigned long long*>(gsrc + off + e * g.es)));
+#else
+                v[e] = gsrc[off + e * g.es];
+#endif
+            } else {
+                v[e] = p[e * g.es];
+            }
         });
         rfft<N2, INV>(v);
         static_for<1, N2>([&](auto ec) {
@@ -502,6 +515,23 @@ __device__ __forceinline__ void fft_lines_rd(float2* base, const Lines g, const 
     }
     __syncthreads();
 }
+// G whose first stage reads its lines from global memory `src` (same layout as base) and leaves the
+// result in base (LDS): the copy into LDS and its barrier fold into the transform.  Two-stage sizes
+// only.  Ends with a barrier.
+template <int N, bool INV, class Epi>
+__device__ __forceinline__ void fft_lines_rd_from(float2* base, const float2* __restrict__ src, const Lines g,
+                                                  const float2* tw, Epi& epi) {
+    using F = LineFFT<N, INV>;
+    static_assert(F::N2 > 1, "two-stage sizes only");
+    const int T = blockDim.x;
+    const int nlines = g.nlines();
+    for (int u = threadIdx.x; u < nlines * F::N1; u += T)
+        F::template stageBp_unit<true>(base, g, tw, u, src);
+    __syncthreads();
+    for (int u = threadIdx.x; u < nlines * F::N2; u += T) F::stageAp_unit(base, g, u, epi);
+    __syncthreads();
+}
+
 #endif
 
 // Host emulation of the in-place variants: mode 1 = F_DR, mode 2 = G.

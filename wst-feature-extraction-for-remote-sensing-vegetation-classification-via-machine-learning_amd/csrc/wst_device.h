@@ -44,8 +44,10 @@ constexpr int kFuseMin = 48;
 constexpr int kFuse1Min = 48;
 constexpr int kFuseGroup = 4;
 // SQ k_o2 of size classes up to this cap: B holds all L paths of the first order-2 level too (host:
-// bcap), so that level runs as one batch instead of L / 2 filter-pair batches
-constexpr int kWholeFirstCap = 48;
+// bcap), so that level runs as one batch instead of L / 2 filter-pair batches (c2 k_o2 j1 = 2
+// 0.160 -> 0.122 ms per step; at the 48 class, j1 = 1, 0.509 -> 0.604: the larger B cuts the
+// workgroups per CU from 7 to 3)
+constexpr int kWholeFirstCap = 24;
 
 constexpr int kMaxLds = 160 * 1024;
 constexpr int kMaxO = 8;  // outputs per thread per generic-DFT chunk
@@ -1799,6 +1801,7 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     if (!do2) return;
 
     // 4. real-input row FFT of (U1 - mean): physical rows 2r, 2r+1 packed as re/im of row 2r
+    //    (packing inside the transform's first stage measured neutral: c2 k_o1 0.728 -> 0.727 ms)
     const int nh = nM1 >> 1;
     for (GridIter it(nN1); it.u < nh; it.next()) {
         float2* a = A + (2 * it.u) * ld1 + it.v;
@@ -1966,11 +1969,18 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     if constexpr (!HG) {
         // 1. half spectrum rows -> LDS, then the column FFTs (rows digit-reversed -> natural)
         float2* Hl = reinterpret_cast<float2*>(smem);
-        if (!(dbg & 1024)) copy_to_lds(Hl, Hg, nM1 * hld);
-        __syncthreads();
-        if (!(dbg & 4))
-            lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(
-                Hl, wstfft::Lines{1, 0, hld, 1, hld}, nM1, tb.twM(j1), id);
+        if constexpr (N1C > 0 && wstfft::LineFFT<(N1C > 0 ? N1C : 2), false>::N2 > 1) {
+            // compile-time two-stage size: the column transform's first stage reads the rows from
+            // the workspace itself (no separate copy pass and barrier; tables ready after one)
+            __syncthreads();
+            wstfft::fft_lines_rd_from<N1C, false>(Hl, Hg, wstfft::Lines{1, 0, hld, 1, hld}, tb.twM(j1), id);
+        } else {
+            if (!(dbg & 1024)) copy_to_lds(Hl, Hg, nM1 * hld);
+            __syncthreads();
+            if (!(dbg & 4))
+                lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(
+                    Hl, wstfft::Lines{1, 0, hld, 1, hld}, nM1, tb.twM(j1), id);
+        }
         if constexpr (N1C > 0) {
             // row N1 = row 0: the tile folds' mirrored taps of bin row u = 0 at alias a = 0
             for (int i = threadIdx.x; i < hld; i += blockDim.x) Hl[nM1 * hld + i] = Hl[i];
