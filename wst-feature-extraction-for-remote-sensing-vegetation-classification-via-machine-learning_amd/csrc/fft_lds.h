@@ -393,7 +393,7 @@ struct LineFFT {
         static_for<0, N2>([&](auto ec) {
             constexpr int e = decltype(ec)::value;
             if constexpr (GL) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(WST_GL_PLAIN)
                 v[e] = __builtin_bit_cast(float2, __builtin_nontemporal_load(
                                                       reinterpret_cast<const unsigned long long*>(gsrc + off + e * g.es)));
 #else

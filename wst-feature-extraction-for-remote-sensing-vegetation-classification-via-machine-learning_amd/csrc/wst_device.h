@@ -48,6 +48,9 @@ constexpr int kFuseGroup = 4;
 // 0.160 -> 0.122 ms per step; at the 48 class, j1 = 1, 0.509 -> 0.604: the larger B cuts the
 // workgroups per CU from 7 to 3)
 constexpr int kWholeFirstCap = 24;
+#ifndef WST_HG_R   // A/B experiment (temporary)
+#define WST_HG_R 2
+#endif
 
 constexpr int kMaxLds = 160 * 1024;
 constexpr int kMaxO = 8;  // outputs per thread per generic-DFT chunk
@@ -2031,7 +2034,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                     fold2_tile_list<N1F, SC>(H, ps, npair, npath, B,
                                              p.taph + p.taph_off[j2 * J + j1] + (l2a >> 1) * NT, p.taps);
                 } else {
-                    fold2_any<HG ? 2 : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2,
+                    fold2_any<HG ? WST_HG_R : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2,
                                           nN2, bx, nM2 + nN2);
                 }
             }
