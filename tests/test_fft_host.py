@@ -70,3 +70,18 @@ def test_inplace_digit_reversed_roundtrip(n, inverse):
     _lib.host_fft_lines(z, n, inverse, 1, 0, rows, ld, 1, 256, mode=2)
     got2 = np.stack([z[r * ld: r * ld + n] for r in range(rows)])
     assert np.abs(got2 - ref).max() / np.abs(ref).max() < tol
+
+
+@pytest.mark.parametrize("n", [n for n in COMPILED if n > 16 and n not in (17,)])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_rd_from_global_equals_inplace(n, inverse):
+    """mode 3 (k_o2's spectrum column transform: G whose first stage reads the workspace rows
+    instead of an LDS copy, csrc/fft_lds.h fft_lines_rd_from) is bitwise mode 2 on the same input,
+    along columns of a half-spectrum-shaped array (nl = hld columns, ls = 1, es = hld)."""
+    rng = np.random.default_rng(200 + n)
+    hld = n // 2 + 1
+    a = (rng.standard_normal(n * hld) + 1j * rng.standard_normal(n * hld)).astype(np.complex64)
+    ref, got = a.copy(), a.copy()
+    _lib.host_fft_lines(ref, n, inverse, 1, 0, hld, 1, hld, 256, mode=2)
+    _lib.host_fft_lines(got, n, inverse, 1, 0, hld, 1, hld, 256, mode=3)
+    assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), n

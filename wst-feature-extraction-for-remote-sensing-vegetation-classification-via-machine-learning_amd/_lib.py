@@ -183,7 +183,8 @@ def default_convention() -> Convention:
 
 def host_fft_lines(data: np.ndarray, n, inverse, nb, bs, nl, ls, es, threads=256, mode=0):
     """In-place host emulation of the device line FFT on a complex64 buffer (test hook).
-    mode 0 natural->natural, 1 natural->digit-reversed, 2 digit-reversed->natural.
+    mode 0 natural->natural, 1 natural->digit-reversed, 2 digit-reversed->natural, 3 = mode 2 with
+    the first stage reading a copy of the input (k_o2's fft_lines_rd_from; two-stage sizes).
     Returns the digit-reversal map (physical position -> logical index)."""
     assert data.dtype == np.complex64 and data.flags.c_contiguous
     perm = np.zeros(n, np.int32)

@@ -551,6 +551,18 @@ inline void fft_lines_inplace_host(float2* base, const Lines g, const float2* tw
     }
 }
 
+// Host emulation of fft_lines_rd_from (G with the first stage reading `src`, two-stage sizes).
+template <int N, bool INV>
+inline void fft_lines_rd_from_host(float2* base, const float2* src, const Lines g, const float2* tw) {
+    using F = LineFFT<N, INV>;
+    EpiIdentity epi;
+    const int nlines = g.nlines();
+    if constexpr (F::N2 > 1) {
+        for (int u = 0; u < nlines * F::N1; ++u) F::template stageBp_unit<true>(base, g, tw, u, src);
+        for (int u = 0; u < nlines * F::N2; ++u) F::stageAp_unit(base, g, u, epi);
+    }
+}
+
 // Host-side digit-reversal map (same split as the device code): logical index at `pos`.
 inline int dr_logical_host(int n, int pos) {
     const int n2 = split_n2(n);

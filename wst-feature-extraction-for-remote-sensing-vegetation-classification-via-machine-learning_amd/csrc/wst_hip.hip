@@ -1563,7 +1563,7 @@ int wst_host_filter_ex(int M, int N, int J, int L, int kind, int j, int l, int r
 
 int wst_host_fft_lines(int n, int inverse, int mode, float* data, int nb, int bs, int nl, int ls,
                        int es, int threads, int* perm) {
-    if (!data || n < 1 || nb < 1 || nl < 1 || threads < 1 || mode < 0 || mode > 2)
+    if (!data || n < 1 || nb < 1 || nl < 1 || threads < 1 || mode < 0 || mode > 3)
         return fail(WST_ERR_INVALID, "bad arguments");
     std::vector<float2> tw(static_cast<size_t>(n));
     for (int k = 0; k < n; ++k) {
@@ -1572,6 +1572,9 @@ int wst_host_fft_lines(int n, int inverse, int mode, float* data, int nb, int bs
     }
     float2* base = reinterpret_cast<float2*>(data);
     const wstfft::Lines g{nb, bs, nl, ls, es};
+    // elements the geometry spans (mode 3 copies them as the global source)
+    const size_t extent = static_cast<size_t>(nb - 1) * bs + static_cast<size_t>(nl - 1) * ls +
+                          static_cast<size_t>(n - 1) * es + 1;
     bool compiled = false;
     switch (n) {
 #define WST_HOST_CASE(NN)                                                                  \
@@ -1580,6 +1583,13 @@ int wst_host_fft_lines(int n, int inverse, int mode, float* data, int nb, int bs
         if (mode == 0) {                                                                   \
             if (inverse) wstfft::fft_lines_host<NN, true>(base, g, tw.data(), threads);    \
             else wstfft::fft_lines_host<NN, false>(base, g, tw.data(), threads);           \
+        } else if (mode == 3) {                                                            \
+            if (wstfft::LineFFT<NN, false>::N2 == 1)                                       \
+                return fail(WST_ERR_UNSUPPORTED, "mode 3 needs a two-stage size");         \
+            const std::vector<float2> src(base, base + extent);                            \
+            for (size_t i = 0; i < extent; ++i) base[i] = make_float2(NAN, NAN);           \
+            if (inverse) wstfft::fft_lines_rd_from_host<NN, true>(base, src.data(), g, tw.data());  \
+            else wstfft::fft_lines_rd_from_host<NN, false>(base, src.data(), g, tw.data()); \
         } else {                                                                           \
             if (inverse) wstfft::fft_lines_inplace_host<NN, true>(base, g, tw.data(), mode); \
             else wstfft::fft_lines_inplace_host<NN, false>(base, g, tw.data(), mode);      \
