@@ -298,9 +298,11 @@ struct EpiIdentity {
     WST_HD float2 operator()(float2 v) const { return v; }
 };
 
-template <int N, bool INV>
+// N2O > 0: use the split N = (N / N2O) x N2O instead of split_n2(N) (a transform whose digit-reversed
+// order only its own consumers see, e.g. the fused order-2 rows)
+template <int N, bool INV, int N2O = 0>
 struct LineFFT {
-    static constexpr int N2 = split_n2(N);
+    static constexpr int N2 = N2O > 0 ? N2O : split_n2(N);
     static constexpr int N1 = N / N2;
     static constexpr int UPT = (N2 <= 4) ? 4 : (N2 <= 8 ? 2 : 1);  // stage-B units per thread
 
@@ -393,7 +395,7 @@ struct LineFFT {
         static_for<0, N2>([&](auto ec) {
             constexpr int e = decltype(ec)::value;
             if constexpr (GL) {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(WST_GL_PLAIN)
+#if defined(__HIP_DEVICE_COMPILE__)
                 v[e] = __builtin_bit_cast(float2, __builtin_nontemporal_load(
                                                       reinterpret_cast<const unsigned long long*>(gsrc + off + e * g.es)));
 #else
@@ -493,9 +495,9 @@ __device__ __forceinline__ void fft_lines_dr(float2* base, const Lines g, const 
     __syncthreads();
 }
 // Stage B alone of F_DR (stage A done by the caller, e.g. fused with a fold).  Ends with a barrier.
-template <int N, bool INV, class Epi>
+template <int N, bool INV, int N2O = 0, class Epi = EpiIdentity>
 __device__ __forceinline__ void fft_lines_dr_stageB(float2* base, const Lines g, Epi& epi) {
-    using F = LineFFT<N, INV>;
+    using F = LineFFT<N, INV, N2O>;
     static_assert(F::N2 > 1, "two-stage sizes only");
     for (int u = threadIdx.x; u < g.nlines() * F::N1; u += blockDim.x) F::stageB_inplace(base, g, u, epi);
     __syncthreads();

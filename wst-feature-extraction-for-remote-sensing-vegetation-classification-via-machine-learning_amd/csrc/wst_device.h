@@ -48,9 +48,12 @@ constexpr int kFuseGroup = 4;
 // 0.160 -> 0.122 ms per step; at the 48 class, j1 = 1, 0.509 -> 0.604: the larger B cuts the
 // workgroups per CU from 7 to 3)
 constexpr int kWholeFirstCap = 24;
-#ifndef WST_HG_R   // A/B experiment (temporary)
-#define WST_HG_R 2
-#endif
+// Row split of the order-2 paths whose s = 2 fold is fused with the rows' stage A (0: split_n2):
+// 48 = 6 x 8 gives the fused phase 384 units of 6 elements per filter pair instead of 288 of 8 on
+// 512 threads.  The columns keep split_n2 (grouped column partials); the S2 pass reads each
+// logical column's partial from its position in the rows' order (cols_modlp RS).
+constexpr int fused_row_n2(int n) { return n == 48 ? 8 : 0; }
+
 
 constexpr int kMaxLds = 160 * 1024;
 constexpr int kMaxO = 8;  // outputs per thread per generic-DFT chunk
@@ -846,7 +849,10 @@ __device__ __forceinline__ void lds_lowpass_taps(float2* U, int rows, int cols, 
 //   2. W[a][q] = sum_k V_k[a][q], written over V_0;
 //   3. S[b][a][c] = sum_q GN[q][c] W[a][q]  (QC lanes per output, shuffle-reduced).
 // Requires oM <= min(kLpOM, 2 RU) (host: fused_lowpass_ok).  Ends with a barrier.
-template <int NN>
+// RS > 0: the rows were transformed with the split N = (NN / RS) x RS (fused_row_n2), so physical
+// column q holds another logical column than GN's rows (split_n2 order) assume: the S pass walks
+// GN's order and reads each column's partial from its position in the rows' order.
+template <int NN, int RS = 0>
 __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, int ld,
                                            const float2* tw, const float* GM, const float* GN,
                                            int oms, int oM, int oN, float scale, float* S,
@@ -947,10 +953,16 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
         const float* f = reinterpret_cast<const float*>(U + b * bs + (a >> 1) * ld) + (a & 1);
         float acc = 0.f;
         for (int q = qc; q < cols; q += QC) {
+            int qr = q;   // position of GN row q's logical column in the rows' order
+            if constexpr (RS > 0) {
+                constexpr int N2d = wstfft::split_n2(NN), N1d = NN / N2d, N1r = NN / RS;
+                const int lg = q / N2d + N1d * (q % N2d);
+                qr = RS * (lg % N1r) + lg / N1r;
+            }
             float wq = 0.f;
             wstfft::static_for<0, NUS>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
-                wq += f[2 * (q + RU * k * ld)];
+                wq += f[2 * (qr + RU * k * ld)];
             });
             acc = fmaf(GN[q * oms + c], wq, acc);
         }
@@ -963,7 +975,7 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
     __syncthreads();
 }
 
-template <int FAM, int K, int HI>
+template <int FAM, int K, int HI, int RS = 0>
 __device__ __forceinline__ void family_cols_modlp(float2* U, int nb, int bs, int rows, int cols,
                                                   int ld, const float2* tw, const float* GM,
                                                   const float* GN, int oms, int oM, int oN,
@@ -972,11 +984,11 @@ __device__ __forceinline__ void family_cols_modlp(float2* U, int nb, int bs, int
     if constexpr (FAM > 0 && NN <= HI && NN <= wstfft::kMaxFamilyN) {
         if constexpr (NN >= 2) {
             if (rows == NN) {
-                cols_modlp<NN>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
+                cols_modlp<NN, RS>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
                 return;
             }
         }
-        family_cols_modlp<FAM, K + 1, HI>(U, nb, bs, rows, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
+        family_cols_modlp<FAM, K + 1, HI, RS>(U, nb, bs, rows, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
     }
 }
 
@@ -1491,7 +1503,7 @@ __device__ __forceinline__ void fold2_s2_rowA(const float2* __restrict__ H, cons
                                               int npair, int npath, float2* __restrict__ B,
                                               const float2* __restrict__ tw) {
     constexpr int N2 = N1 / 2, HLD = N1 / 2 + 1, LD2 = N2 | 1, PSLOT = N2 * LD2, PST = N1 * N1;
-    using F = wstfft::LineFFT<N2, true>;
+    using F = wstfft::LineFFT<N2, true, fused_row_n2(N2)>;
     static_assert(F::N2 > 1, "two-stage row sizes only");
     constexpr int NA = F::N1, NB = F::N2, UNITS = N2 * NB;
     const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, npair * PST * 8);
@@ -2034,7 +2046,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                     fold2_tile_list<N1F, SC>(H, ps, npair, npath, B,
                                              p.taph + p.taph_off[j2 * J + j1] + (l2a >> 1) * NT, p.taps);
                 } else {
-                    fold2_any<HG ? WST_HG_R : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2,
+                    fold2_any<HG ? 2 : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2,
                                           nN2, bx, nM2 + nN2);
                 }
             }
@@ -2044,7 +2056,8 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                 // rows, then the column pass fused with |.| and the S2 low-pass
                 if (!(dbg & 16)) {
                     if constexpr (FUSE)
-                        wstfft::fft_lines_dr_stageB<(N1F > 0 ? N1F / 2 : 2), true>(
+                        wstfft::fft_lines_dr_stageB<(N1F > 0 ? N1F / 2 : 2), true,
+                                                    fused_row_n2(N1F > 0 ? N1F / 2 : 2)>(
                             B, wstfft::Lines{npath, pslot, nM2, ld2, 1}, id);
                     else
                         lds_fft_lines<FN, 0, PHI, kDR, true>(
@@ -2053,7 +2066,8 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                 const int k0 = kbase + (j2 - j1 - 1) * L + l2a;
                 float* outd = pooled ? nullptr : out + (img * p.K + k0) * (oM * oN);
                 if (!(dbg & 64))
-                    family_cols_modlp<FM, 0, PHI>(B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
+                    family_cols_modlp<FM, 0, PHI, FUSE ? fused_row_n2(N1F > 0 ? N1F / 2 : 2) : 0>(
+                                                       B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
                                                        tb.gM(j2), tb.gN(j2), oms, oM, oN,
                                                        scale2, S, outd);
                 if (!outd) emit(S, npath, k0, img, p.K, oM, oN, out, pooled);
