@@ -85,3 +85,24 @@ def test_rd_from_global_equals_inplace(n, inverse):
     _lib.host_fft_lines(ref, n, inverse, 1, 0, hld, 1, hld, 256, mode=2)
     _lib.host_fft_lines(got, n, inverse, 1, 0, hld, 1, hld, 256, mode=3)
     assert np.array_equal(got.view(np.uint64), ref.view(np.uint64)), n
+
+
+@pytest.mark.parametrize("nn,rs", [(48, 8)])
+def test_fused_row_split_column_remap(nn, rs):
+    """The S2 pass of the 48^2 order-2 paths (csrc/wst_device.h cols_modlp RS) walks the tap matrix
+    GN in the split_n2 digit-reversed order and reads each logical column's partial from its place
+    in the rows' order (split (nn / rs) x rs, fused_row_n2): the remap must land every GN row on the
+    physical column that holds the same logical column.  The library's own digit-reversal map
+    (mode 1 perm) fixes the split_n2 side."""
+    x = np.zeros(nn, np.complex64)
+    perm_default = _lib.host_fft_lines(x, nn, True, 1, 0, 1, nn, 1, 64, mode=1)
+    n2d = next(d for d in range(int(nn ** 0.5), 0, -1) if nn % d == 0)
+    n1d, n1r = nn // n2d, nn // rs
+    seen = set()
+    for q in range(nn):
+        lg = q // n2d + n1d * (q % n2d)
+        assert lg == perm_default[q]
+        qr = rs * (lg % n1r) + lg // n1r
+        assert qr // rs + n1r * (qr % rs) == lg        # rows' digit-reversed order
+        seen.add(qr)
+    assert seen == set(range(nn))
