@@ -1515,7 +1515,13 @@ __device__ __forceinline__ void fold2_s2_rowA(const float2* __restrict__ H, cons
     for (int w = w0; w < npair * UNITS; w += blockDim.x) {
         const int pr = w / UNITS;
         const int r = w - pr * UNITS;
-        const int u = r / NB, n2 = r - u * NB;
+        const int g = r / NB, n2 = r - g * NB;
+        // row of lane group g (NB lanes of one row): with NB = 8 a half-wave holds 4 groups; taking
+        // rows h, h + 8, h + 16, h + 24 for them puts their stride-HLD / stride-LD2 LDS rows (odd,
+        // = 17 mod 32 float2) on disjoint banks (the first 32 rows; the rest keep their order)
+        int u = g;
+        if constexpr (NB == 8 && N2 >= 32 && (UNITS % 32) == 0)
+            if (g < 32) u = 8 * (g & 3) + (g >> 2);
         const int db = (u * HLD + n2) * 8;
         const int mb = ((N2 - u) * HLD + (NB - n2)) * 8;
         const int fo = (u * N1 + n2 + pr * PST) * 8;   // lanes of a wave may straddle pairs
