@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 99
 mkdir -p gpurun_out/$tag
 for lib in "$@"; do
   d=gpurun_out/$tag/${lib%.so}
-  WST_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o run -- python3 tools/kernel_ms.py 1536 > $d.log 2>&1 || { echo "$lib failed"; tail -5 $d.log; exit 99; }
+  AB_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $d -o run -- python3 tools/kernel_ms.py 1536 > $d.log 2>&1 || { echo "$lib failed"; tail -5 $d.log; exit 99; }
   f=$(find $d -name "*kernel_stats.csv" | head -1)
   python3 tools/kstats.py "$rx" "$f"
 done

@@ -2,7 +2,7 @@
 
 Needs the diagnostic build (the production library ignores WST_DEBUG_SKIP):
     make -C <pkg>/csrc OUT=../libwst_hip_diag.so OBJ=../build_diag EXTRA=-DWST_DIAG -j16
-and runs it through WST_LIB=libwst_hip_diag.so."""
+and loads it through _lib.use_library (ABL_LIB names the file)."""
 import os, subprocess, sys, json
 masks = {"full": 0, "no_o1_fold": 128, "no_o1_ifft": 1, "no_S1": 2, "no_U1_fft": 4, "no_o2_fold": 8,
          "no_o2_ifft": 16, "no_o2_lowpass": 64, "no_order2_paths": 8 | 16 | 64,
@@ -16,6 +16,7 @@ import os, sys, json
 sys.path.insert(0, os.getcwd())
 import numpy as np, torch, wst_amd
 from wst_amd import _lib
+_lib.use_library(os.environ["ABL_LIB"])
 B, M, J = (int(v) for v in os.environ.get("WST_KM_GEOM", "3072,64,4").split(","))
 x = torch.from_numpy(np.random.default_rng(1).integers(0,256,(B,M,M),dtype=np.uint8).astype(np.float32)/255).cuda()
 plan = _lib.Plan(M,M,J,8)
@@ -31,7 +32,7 @@ print(json.dumps([a/3 for a in acc]))
 '''
 res = {}
 for name, m in masks.items():
-    env = dict(os.environ, WST_DEBUG_SKIP=str(m), WST_LIB=LIB)
+    env = dict(os.environ, WST_DEBUG_SKIP=str(m), ABL_LIB=LIB)
     r = subprocess.run([sys.executable, "-c", child], env=env, capture_output=True, text=True, timeout=300)
     line = [l for l in r.stdout.splitlines() if l.startswith("[")]
     res[name] = json.loads(line[-1]) if line else r.stderr[-300:]

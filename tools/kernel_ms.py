@@ -4,6 +4,8 @@ import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch, wst_amd  # noqa: F401
 from wst_amd import _lib
+if os.environ.get("AB_LIB"):          # A/B variant build in the package dir (tools/variant.sh)
+    _lib.use_library(os.environ["AB_LIB"])
 # geometry: env WST_KM_GEOM="planes,M,J" (default the c2 step: 3072 planes of 64^2, J=4)
 B, M, J = (int(v) for v in os.environ.get("WST_KM_GEOM", "3072,64,4").split(","))
 x = torch.from_numpy(np.random.default_rng(1).integers(0, 256, (B, M, M), dtype=np.uint8).astype(np.float32) / 255).cuda()
@@ -25,6 +27,6 @@ for chunk in [int(a) for a in sys.argv[1:]] or [2048]:
         ms = plan.forward_profiled(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st, nslot)
         acc = [a + b for a, b in zip(acc, ms)]
     acc = [round(a / 5, 3) for a in acc]
-    print(os.environ.get("WST_LIB", "default"), f"chunk={chunk} wall={wall:.3f} ms",
+    print(os.environ.get("AB_LIB", "default"), f"chunk={chunk} wall={wall:.3f} ms",
           "prep", acc[0], "o1", acc[1:1 + J], "o2", acc[1 + J:], "sum", round(sum(acc), 3), flush=True)
     del ws

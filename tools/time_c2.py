@@ -3,6 +3,9 @@ import argparse, sys, os, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 import wst_amd
+from wst_amd import _lib
+if os.environ.get("AB_LIB"):          # A/B variant build in the package dir (tools/variant.sh)
+    _lib.use_library(os.environ["AB_LIB"])
 from wst_amd.frontend import scatter_device
 ap = argparse.ArgumentParser()
 ap.add_argument("--B", type=int, default=1024); ap.add_argument("--C", type=int, default=3)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build a library variant that differs only in one family pair's kernels (A/B dev tool):
-#   [PAIR=17_17] tools/variant.sh <name> <extra hipcc flags...>   ->  <pkg>/var_<name>.so  (WST_LIB=var_<name>.so)
+#   [PAIR=17_17] tools/variant.sh <name> <extra hipcc flags...>   ->  <pkg>/var_<name>.so  (AB_LIB=var_<name>.so)
 # (-DWST_DIAG variants also need the host side: VARIANT_HOST=1 recompiles wst_hip.hip with the flags;
 #  HOST_ONLY=1: only wst_hip.hip with the flags, production kernels -- e.g. the env A/B knobs of -DWST_DIAG)
 name=$1; shift
@@ -21,4 +21,4 @@ if [ -n "$VARIANT_HOST" ]; then
   objs="$(echo $objs | tr ' ' '\n' | grep -v wst_hip.o) ../../build_var/wst_hip_$name.o"
 fi
 /opt/rocm/bin/hipcc $F -shared -o ../var_$name.so $objs
-echo built $pkg/var_$name.so "(WST_LIB=var_$name.so)"
+echo built $pkg/var_$name.so "(AB_LIB=var_$name.so)"

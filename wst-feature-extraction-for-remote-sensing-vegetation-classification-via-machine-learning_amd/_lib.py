@@ -12,8 +12,9 @@ import threading
 
 import numpy as np
 
-LIB_NAME = os.environ.get("WST_LIB", "libwst_hip.so")   # WST_LIB: A/B-test builds in the pkg dir
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.path.basename(LIB_NAME))
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "libwst_hip.so"
+LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
 
 WST_OK, WST_ERR_INVALID, WST_ERR_UNSUPPORTED, WST_ERR_HIP, WST_ERR_NOMEM = 0, 1, 2, 3, 4
 ABI_VERSION = 2
@@ -33,6 +34,18 @@ EXPORTS = (
 
 _lib = None
 _lock = threading.Lock()
+
+
+def use_library(name: str) -> None:
+    """Development tools only (tools/kernel_ms.py, tools/ablate.py): load the variant build
+    `name` (a file in the package directory, e.g. a WST_DIAG build) instead of libwst_hip.so.
+    Must run before the first load(); the product path never calls it, and no environment
+    variable selects a library."""
+    global LIB_NAME, LIB_PATH
+    if _lib is not None:
+        raise RuntimeError(f"{LIB_NAME} is already loaded")
+    LIB_NAME = os.path.basename(name)
+    LIB_PATH = os.path.join(PKG_DIR, LIB_NAME)
 
 
 class Convention(ctypes.Structure):
