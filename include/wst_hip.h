@@ -143,6 +143,28 @@ int wst_forward_profiled(const wst_plan* plan, const float* d_in, int64_t nbatch
                          float* kernel_ms, int n_kernel_ms);
 
 /*
+ * Kernel-variant introspection (test hooks; no kymatio counterpart).  Every launch of a forward
+ * is a "site" of 12 int32 words: word 0 the kernel instantiation (family pair, size class / line
+ * length, SQ, HG), word 1 the body it dispatches to at run time (compile-time sizes, output-map
+ * and L specialisations, fold and low-pass forms), words 2.. the branch of each order-2 level
+ * (k_o2).  Encoding: wst_device.h tr_* (decoded by wst_amd/variants.py).
+ *   wst_plan_variants     : the sites one chunk of `plan` launches, from the host mirror of the
+ *                           kernels' dispatch (no GPU work).
+ *   wst_describe_variants : the same for a geometry, without a GPU (a host-only plan: no
+ *                           device allocation, zero-valued filters of the right shapes).
+ *   wst_plan_trace        : enable (1) / disable (0) the device trace: every later forward's
+ *                           launches record the words they actually ran.
+ *   wst_plan_read_trace   : copy the device trace (synchronises the device); *nwords = the
+ *                           plan's site count x 12.
+ * out may be NULL for a size query in the first two (then only *nwords is set).
+ */
+int wst_plan_variants(const wst_plan* plan, int32_t* out, int64_t max_words, int64_t* nwords);
+int wst_describe_variants(int M, int N, int J, int L, int max_order, int32_t* out, int64_t max_words,
+                          int64_t* nwords);
+int wst_plan_trace(wst_plan* plan, int enable);
+int wst_plan_read_trace(const wst_plan* plan, int32_t* out, int64_t max_words, int64_t* nwords);
+
+/*
  * Host-only filter inspection (no GPU needed; used by the CPU test-suite to pin the library's
  * float64 filter construction against the oracle).  kind:
  *   0 = psi_{j,l} Fourier level r        -> (PM>>r) x (PN>>r) doubles

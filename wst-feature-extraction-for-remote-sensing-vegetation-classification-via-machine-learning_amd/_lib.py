@@ -29,7 +29,8 @@ EXPORTS = (
     "wst_forward_profiled", "wst_host_filter", "wst_host_filter_ex", "wst_host_fft_lines",
     "wst_salt_pepper_counts", "wst_noise_apply", "wst_noise_generate", "wst_advanced_stats",
     "wst_patch_generate", "wst_u8_to_chw", "wst_probe_copy", "wst_probe_fma",
-    "wst_aux_last_error",
+    "wst_aux_last_error", "wst_plan_variants", "wst_describe_variants", "wst_plan_trace",
+    "wst_plan_read_trace",
 )
 
 _lib = None
@@ -154,6 +155,15 @@ def load() -> ctypes.CDLL:
                                         ctypes.POINTER(ctypes.c_double), c_i64]
         lib.wst_host_fft_lines.restype = c_int
         lib.wst_host_fft_lines.argtypes = [c_int, c_int, c_int, c_vp] + [c_int] * 6 + [c_vp]
+        i64p = ctypes.POINTER(c_i64)
+        lib.wst_plan_variants.restype = c_int
+        lib.wst_plan_variants.argtypes = [c_vp, c_vp, c_i64, i64p]
+        lib.wst_describe_variants.restype = c_int
+        lib.wst_describe_variants.argtypes = [c_int] * 5 + [c_vp, c_i64, i64p]
+        lib.wst_plan_trace.restype = c_int
+        lib.wst_plan_trace.argtypes = [c_vp, c_int]
+        lib.wst_plan_read_trace.restype = c_int
+        lib.wst_plan_read_trace.argtypes = [c_vp, c_vp, c_i64, i64p]
         v = lib.wst_abi_version()
         if v != ABI_VERSION:
             raise RuntimeError(f"{LIB_NAME} ABI version {v} != expected {ABI_VERSION}; rebuild it")
@@ -186,6 +196,18 @@ def host_filter(M, N, J, L, kind, j, l, r, size, convention=None) -> np.ndarray:
     check(load().wst_host_filter_ex(M, N, J, L, kind, j, l, r, _conv_ptr(convention),
                                     out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), size))
     return out
+
+
+def describe_variants(M, N, J, L, max_order=2) -> np.ndarray:
+    """Trace words (sites x 12, int32) one chunk of a plan for this geometry launches, from the
+    library's host mirror of the kernels' dispatch; no GPU needed (wst_describe_variants)."""
+    lib = load()
+    n = ctypes.c_int64()
+    check(lib.wst_describe_variants(int(M), int(N), int(J), int(L), int(max_order), None, 0, ctypes.byref(n)))
+    out = np.zeros(max(n.value, 1), np.int32)
+    check(lib.wst_describe_variants(int(M), int(N), int(J), int(L), int(max_order), out.ctypes.data,
+                                    out.size, ctypes.byref(n)))
+    return out[:n.value].reshape(-1, 12)
 
 
 def default_convention() -> Convention:
@@ -266,6 +288,26 @@ class Plan:
                                           ctypes.c_void_p(d_ws or None), int(ws_bytes),
                                           ctypes.c_void_p(stream or None), ms, nslots))
         return list(ms)
+
+    def variants(self) -> np.ndarray:
+        """Host-mirror trace words of one chunk (sites x 12, wst_plan_variants)."""
+        n = ctypes.c_int64()
+        check(load().wst_plan_variants(self._h, None, 0, ctypes.byref(n)))
+        out = np.zeros(max(n.value, 1), np.int32)
+        check(load().wst_plan_variants(self._h, out.ctypes.data, out.size, ctypes.byref(n)))
+        return out[:n.value].reshape(-1, 12)
+
+    def trace(self, enable: bool) -> None:
+        """Enable / disable the device variant trace (wst_plan_trace)."""
+        check(load().wst_plan_trace(self._h, 1 if enable else 0))
+
+    def read_trace(self) -> np.ndarray:
+        """Device trace words of the last traced forward (sites x 12, wst_plan_read_trace)."""
+        n = ctypes.c_int64()
+        check(load().wst_plan_variants(self._h, None, 0, ctypes.byref(n)))
+        out = np.zeros(max(n.value, 1), np.int32)
+        check(load().wst_plan_read_trace(self._h, out.ctypes.data, out.size, ctypes.byref(n)))
+        return out[:n.value].reshape(-1, 12)
 
     def close(self):
         if getattr(self, "_h", None) is not None and _lib is not None:

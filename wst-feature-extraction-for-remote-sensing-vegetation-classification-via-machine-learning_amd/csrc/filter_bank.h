@@ -76,5 +76,8 @@ struct FilterBank {
 // Build the full bank (float64).  Throws std::runtime_error on internal inconsistency (e.g. a
 // phi spectrum that is not separable to 1e-12, which would invalidate the separable low-pass).
 FilterBank build_filter_bank(const Geometry& g, const FilterConvention& conv = kKymatio030);
+// Host-only plans (wst_describe_variants): the low-pass factors with their shapes (zero-valued)
+// and no band-pass filters -- every structural decision of a plan, no float64 construction.
+FilterBank shape_filter_bank(const Geometry& g);
 
 }  // namespace wst

@@ -96,6 +96,7 @@ struct DevParams {
     const int4* taph;
     const int* taph_off;
     const int2* taps;
+    int* vtrace;                  // variant trace (wst_plan_trace, tests); nullptr: off
 };
 
 // Per-launch LDS layout (byte offsets) and the table slices copied into LDS.
@@ -119,7 +120,67 @@ struct LdsLayout {
     int hext;               // resident levels: an item's half spectrum in the workspace holds
                             // nM1 + 1 rows (row nM1 = row 0 for the tile folds' mirrored taps;
                             // written by an exporting k_o1, formed in LDS by k_o2 otherwise)
+    int tslot;              // variant-trace site of this launch (DevParams::vtrace)
 };
+
+// ------------------------------------------------------------------------------------------
+// Variant trace (tests: wst_plan_trace / wst_describe_variants, include/wst_hip.h).  With
+// DevParams::vtrace set, workgroup 0 of every traced launch writes kTraceW words at its site
+// (LdsLayout::tslot / BigArgs::tslot): word 0 the kernel instantiation, word 1 the body it
+// dispatched to at run time, words 2.. (k_o2) the branch of each order-2 level it ran (index
+// j2 - j1 - 1).  The host mirror in wst_hip.hip (describe_chunk) predicts the same words from the
+// plan alone; tests/test_variants*.py check the two agree on the GPU and that the GPU oracle tests'
+// geometries reach every variant a geometry can select.  Plain vector stores by one lane.
+// ------------------------------------------------------------------------------------------
+constexpr int kTraceW = 12;
+constexpr int kTraceSites = 512;
+enum TraceKind : int { kTkPrep = 1, kTkO1 = 2, kTkO2 = 3, kTkBigRows = 4, kTkBigCols = 5 };
+// low-pass forms: tap matrices (SQ), MFMA with compile-time K, MFMA, 1-D taps
+enum TraceLp : int { kLpTap = 0, kLpMfmaRc = 1, kLpMfma = 2, kLpPlain = 3 };
+// order-2 fold forms
+enum TraceFold : int { kFdFused = 1, kFdTileS2 = 2, kFdTileList = 3, kFdDenseS2 = 4, kFdBox = 5 };
+constexpr int tr_log2(int v) {
+    int l = 0;
+    while (v > 1) {
+        v >>= 1;
+        ++l;
+    }
+    return l;
+}
+// word 0: kind | family M | family N | size class (or staged line length) | SQ | HG (INV)
+constexpr int tr_kernel(int kind, int fm, int fn, int cap, int sq, int hg) {
+    return (kind << 28) | (fm << 22) | (fn << 16) | (cap << 4) | (sq << 1) | hg;
+}
+// k_prep body: compile-time size | low-pass form
+constexpr int tr_prep(int pc, int lp) { return pc | (lp << 8); }
+// k_o1 body: OC | compile-time level size | fused s = 1 fold + row stage A | S1 low-pass form |
+// order 2 follows | exports the full spectrum | order-1 fold form (0 fused, 1 s=1, 2 s=2, 3 box,
+// 4 s=4, 5 runtime s)
+constexpr int tr_o1(int oc, int n1c, int fused1, int lp, int do2, int exp, int fold) {
+    return oc | (n1c << 4) | (fused1 << 12) | (lp << 13) | (do2 << 15) | (exp << 16) | (fold << 17);
+}
+// k_o2 body: OC | LC | compile-time level size | spectrum load (0 HBM fold, 1 first column stage
+// from the workspace, 2 copy) | level-dispatch branch (1 N1C, 2-4 HG compile-time / exported /
+// runtime after a big level, 5-6 exported-spectrum compile-time / runtime, 7 runtime)
+constexpr int tr_o2(int oc, int lc, int n1c, int spec, int branch) {
+    return oc | (lc << 4) | (n1c << 9) | (spec << 17) | (branch << 19);
+}
+// order-2 level: valid | log2 s | low-pass form | fold form | compile-time path size | log2 SC
+// (0: runtime) | PB | j2
+constexpr int tr_level(int j2, int pb, int sc, int nc, int fold, int lp, int s2) {
+    return 1 | (tr_log2(s2) << 1) | (lp << 5) | (fold << 7) | (nc << 10) | ((sc ? tr_log2(sc) : 0) << 18) |
+           (pb << 21) | (j2 << 26);
+}
+// staged passes: mode | fold_all | order-1 fold form (1 s = 1, 2 s > 1) | box fold | wide maps |
+// tap matrix in LDS | U stored
+constexpr int tr_big(int mode, int fold_all, int fold1, int box, int wide, int glds, int ustore) {
+    return mode | (fold_all << 2) | (fold1 << 3) | (box << 5) | (wide << 6) | (glds << 7) | (ustore << 8);
+}
+__device__ __forceinline__ void trace_word(const DevParams& p, int tslot, int k, int v) {
+    if (p.vtrace && tslot >= 0 && tslot < kTraceSites && threadIdx.x == 0 && blockIdx.x == 0 &&
+        blockIdx.y == 0)
+        p.vtrace[tslot * kTraceW + k] = v;
+}
 
 // ------------------------------------------------------------------------------------------
 // helpers
@@ -984,7 +1045,9 @@ __device__ __forceinline__ void family_cols_modlp(float2* U, int nb, int bs, int
     if constexpr (FAM > 0 && NN <= HI && NN <= wstfft::kMaxFamilyN) {
         if constexpr (NN >= 2) {
             if (rows == NN) {
-                cols_modlp<NN, RS>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
+                // RS belongs to the fused 48-point rows only (the other sizes never meet it)
+                constexpr int RSN = fused_row_n2(NN) == RS ? RS : 0;
+                cols_modlp<NN, RSN>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
                 return;
             }
         }
@@ -1669,6 +1732,8 @@ __device__ __forceinline__ void prep_body(unsigned char* smem, const DevParams& 
     const long long img = img0 + local;
     const int inM = p.pre_pad ? PM : p.M, inN = p.pre_pad ? PN : p.N;
     const float* x = in + local * inM * inN;
+    trace_word(p, lay.tslot, 0, tr_kernel(kTkPrep, FM, FN, 0, 0, 0));
+    trace_word(p, lay.tslot, 1, tr_prep(PC, wide_lowpass(p) ? (mfma_rc_ok<PC>() ? kLpMfmaRc : kLpMfma) : kLpPlain));
     float part = 0.f;
     for (GridIter it(PN); it.u < PM; it.next()) {
         const int su = p.pre_pad ? it.u : reflect_index(it.u - p.padTop, p.M);
@@ -1779,6 +1844,13 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     // 0.78 -> 0.79, so the exported-spectrum kernels keep the separate fold)
     constexpr bool FUSE1 = SQ && N1C >= kFuse1Min && wstfft::LineFFT<(N1C > 0 ? N1C : 2), true>::N2 > 1;
     const bool fused1 = FUSE1 && j1 == 0;
+    {
+        const int s1 = 1 << j1;
+        const int f1 = fused1 ? 0 : s1 == 1 ? 1 : s1 == 2 ? 2 : use_box1 ? 3 : s1 == 4 ? 4 : 5;
+        const int lp1 = SQ ? kLpTap : wide_lowpass(p) ? (mfma_rc_ok<N1C>() ? kLpMfmaRc : kLpMfma) : kLpPlain;
+        trace_word(p, lay.tslot, 0, tr_kernel(kTkO1, FM, FN, MAXN, SQ, 0));
+        trace_word(p, lay.tslot, 1, tr_o1(OC, N1C, fused1 ? 1 : 0, lp1, do2 ? 1 : 0, lay.export_full, f1));
+    }
     EpiModulus mod1{1.f / (static_cast<float>(PM) * static_cast<float>(PN)), 0.f};
     if (fused1) {
         if constexpr (FUSE1) {
@@ -1986,6 +2058,26 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     const long long img = img0 + local;
     const float2* Hg = hexp + item * hspec_stride(nM1, hld, lay.hext);
     const float2* H = HG ? Hg : reinterpret_cast<const float2*>(smem);
+    {
+        constexpr int spec = HG ? 0 : (N1C > 0 && wstfft::LineFFT<(N1C > 0 ? N1C : 2), false>::N2 > 1) ? 1 : 2;
+        int branch = 7;
+        if constexpr (N1C > 0) {
+            branch = 1;
+        } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {
+            constexpr int N2C = unique_level(FM, MAXN);
+            branch = (j2first == j1 + 1 && (PM >> j1) == N2C && PM == PN) ? 2 : (PM >> j2first) == N2C ? 3 : 4;
+        } else if constexpr (!SQ && HG == 1 && FM == FN && FM > 0) {
+            branch = 6;
+            if (PM == PN && j2first == j1 + 1)
+                wstfft::static_for<0, 8>([&](auto mc) {
+                    constexpr int N1X = FM << decltype(mc)::value;
+                    if constexpr (N1X <= MAXN && N1X > prev_cap(MAXN))
+                        if ((PM >> j1) == N1X) branch = 5;
+                });
+        }
+        trace_word(p, lay.tslot, 0, tr_kernel(kTkO2, FM, FN, MAXN, SQ, HG));
+        trace_word(p, lay.tslot, 1, tr_o2(OC, LC, N1C, spec, branch));
+    }
 
     if constexpr (!HG) {
         // 1. half spectrum rows -> LDS, then the column FFTs (rows digit-reversed -> natural)
@@ -2029,6 +2121,14 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
         const int ld2 = odd_ld(nN2);
         const int pslot = nM2 * ld2;
         const int s2 = 1 << (j2 - j1);
+        {
+            constexpr int fk = FUSE ? kFdFused : (N1F > 0 && SC == 2) ? kFdTileS2
+                             : (N1F > 0 && (SC == 4 || SC == 8)) ? kFdTileList : 0;
+            const int lpk = SQ ? kLpTap : wide_lowpass(p) ? (mfma_rc_ok<NC>() ? kLpMfmaRc : kLpMfma) : kLpPlain;
+            if (2 + (j2 - j1 - 1) < kTraceW)
+                trace_word(p, lay.tslot, 2 + (j2 - j1 - 1),
+                       tr_level(j2, PB, SC, NC, fk ? fk : (s2 == 2 ? kFdDenseS2 : kFdBox), lpk, s2));
+        }
         int pb = lay.bcap / pslot;                 // paths per batch (multiple of 2)
         pb = PB ? PB : max(2, min(pb & ~1, 2 * nq));
 #pragma unroll 1

@@ -22,6 +22,7 @@
 
 #include "filter_bank.h"
 #include "wst_hip.h"
+#include "wst_compiled.h"
 #include "wst_launch.h"
 
 using wstdev::DevParams;
@@ -138,6 +139,9 @@ void threads_override(const char* env, std::vector<int>& v) {
 struct wst_plan {
     wst::Geometry g;
     int device = 0;
+    bool host_only = false;     // wst_describe_variants: structure only, no device allocations
+    int* d_trace = nullptr;     // variant trace buffer (wst_plan_trace)
+    std::vector<int> box1_l0;   // per scale j: box1_off of (j, l = 0) (host mirror of k_o1)
     DevParams dp{};
     // device allocations
     float* d_psi = nullptr;
@@ -220,6 +224,11 @@ namespace {
 
 void free_plan(wst_plan* p) {
     if (!p) return;
+    if (p->host_only) {
+        delete p;
+        return;
+    }
+    (void)hipFree(p->d_trace);
     (void)hipFree(p->d_psi);
     (void)hipFree(p->d_psi_off);
     (void)hipFree(p->d_lp);
@@ -367,6 +376,10 @@ int cyclic_window(const std::vector<char>& hit) {
     return start | (len << 8);
 }
 
+int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
+                const wst_filter_convention* conv_in, bool device, wst_plan** out);
+std::vector<int> describe_chunk(const wst_plan* pl);
+
 // C-ABI convention -> host struct (NULL = kymatio 0.3.0 as recalled); false on a bad value.
 bool to_convention(const wst_filter_convention* c, wst::FilterConvention& out) {
     out = wst::kKymatio030;
@@ -404,6 +417,19 @@ int wst_plan_create(int M, int N, int J, int L, int max_order, int pre_pad, wst_
 
 int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
                        const wst_filter_convention* conv_in, wst_plan** out) {
+    return create_plan(M, N, J, L, max_order, pre_pad, conv_in, true, out);
+}
+
+}  // extern "C"
+
+namespace {
+
+// device = false: a host-only plan (wst_describe_variants): every structural decision of
+// wst_plan_create_ex (families, SQ, staging, layouts, export, launch shapes) on a zero-valued
+// filter bank of the right shapes, no HIP call; only the host mirror of the launch sequence may
+// read it.
+int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
+                const wst_filter_convention* conv_in, bool device, wst_plan** out) {
     if (!out) return fail(WST_ERR_INVALID, "out is NULL");
     *out = nullptr;
     if (J < 1) return fail(WST_ERR_INVALID, "J must be >= 1 (kymatio needs phi level 0)");
@@ -447,7 +473,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     }
     wst::FilterBank fb;
     try {
-        fb = wst::build_filter_bank(g, conv);
+        fb = device ? wst::build_filter_bank(g, conv) : wst::shape_filter_bank(g);
     } catch (const std::exception& e) {
         return fail(WST_ERR_UNSUPPORTED, e.what());
     }
@@ -455,7 +481,8 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     std::unique_ptr<wst_plan, void (*)(wst_plan*)> plan(new (std::nothrow) wst_plan(), free_plan);
     if (!plan) return fail(WST_ERR_NOMEM, "host allocation failed");
     plan->g = g;
-    WST_HIP_CHECK(hipGetDevice(&plan->device));
+    plan->host_only = !device;
+    if (device) WST_HIP_CHECK(hipGetDevice(&plan->device));
 
     plan->fam_m = family_of(g.PM);
     plan->fam_n = family_of(g.PN);
@@ -483,7 +510,8 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     // order-1 filters psi_{j,l} (fp32 real), every kymatio level
     std::vector<float> psi;
     std::vector<long long> psi_off(static_cast<size_t>(J) * L * J, -1);
-    for (int j = 0; j < J; ++j)
+    // (host-only plans skip the value-only tables below: filters, boxes, tap lists)
+    for (int j = 0; j < J && device; ++j)
         for (int l = 0; l < L; ++l) {
             const auto& lev = fb.psi[static_cast<size_t>(j) * L + l];
             for (int r = 0; r < static_cast<int>(lev.size()); ++r) {
@@ -508,7 +536,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     const int nq = (L + 1) / 2;
     std::vector<float2> psi2;
     std::vector<long long> psi2_off(static_cast<size_t>(J) * J * nq, -1);
-    if (max_order >= 2) {
+    if (max_order >= 2 && device) {
         for (int j2 = 1; j2 < J; ++j2)
             for (int r = 0; r < j2 && r < wst::psi_levels(j2, J); ++r)
                 for (int q = 0; q < nq; ++q) {
@@ -527,7 +555,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     // alias boxes of the order-2 pairs (see fold2): per (j2, r) all pairs, stride nM2 + nN2
     std::vector<int> box;
     std::vector<int> box_off(static_cast<size_t>(J) * J, 0);
-    if (max_order >= 2) {
+    if (max_order >= 2 && device) {
         for (int j2 = 1; j2 < J; ++j2)
             for (int r = 0; r < j2 && r < wst::psi_levels(j2, J); ++r) {
                 box_off[static_cast<size_t>(j2) * J + r] = static_cast<int>(box.size());
@@ -570,7 +598,7 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     std::vector<int> taph, taps;
     std::vector<int> taph_off(static_cast<size_t>(J) * J, 0);
     size_t psi2_zero = 0;   // float2 index of the zero block (dummy taps)
-    if (max_order >= 2 && g.PM == g.PN) {
+    if (max_order >= 2 && g.PM == g.PN && device) {
         psi2_zero = psi2.size();
         psi2.resize(psi2.size() + static_cast<size_t>(g.PM) * g.PM / 2 + 64, make_float2(0.f, 0.f));
         for (int j2 = 1; j2 < J; ++j2)
@@ -630,6 +658,11 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     std::vector<int> box1_off(static_cast<size_t>(J) * L, -1);
     for (int j = 2; j < J; ++j)
         for (int l = 0; l < L; ++l) {
+            if (!device) {   // host-only plan: whether a box exists is all the mirror reads
+                const char* e = diag_env("WST_BOX");
+                if (!(e && std::atoi(e) == 0)) box1_off[static_cast<size_t>(j) * L + l] = 0;
+                continue;
+            }
             const int sa = 1 << j, nM1 = g.PM >> j, nN1 = g.PN >> j;
             const auto& f = fb.psi[static_cast<size_t>(j) * L + l][0];
             double mx = 0.0;
@@ -760,30 +793,31 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     }
 
     int rc;
-    if ((rc = upload(&plan->d_psi, psi)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_psi_off, psi_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_lp, lp)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_lp_off, t.lp_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_tw, tw)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_tw_off, t.tw_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_o2, o2)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_psi2, psi2)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_psi2_off, psi2_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_perm, perm)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_perm_off, t.perm_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_box, box)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_box_off, box_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_box1_off, box1_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_taph, taph)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_taph_off, taph_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_taps, taps)) != WST_OK) return rc;
+    const auto up = [&](auto** dst, const auto& src) { return device ? upload(dst, src) : WST_OK; };
+    if ((rc = up(&plan->d_psi, psi)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_psi_off, psi_off)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_lp, lp)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_lp_off, t.lp_off)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_tw, tw)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_tw_off, t.tw_off)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_o2, o2)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_psi2, psi2)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_psi2_off, psi2_off)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_perm, perm)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_perm_off, t.perm_off)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_box, box)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_box_off, box_off)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_box1_off, box1_off)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_taph, taph)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_taph_off, taph_off)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_taps, taps)) != WST_OK) return rc;
     plan->psi2_off_host = psi2_off;
     plan->box_off_host = box_off;
-    if ((rc = upload(&plan->d_lpt, lpt)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_lpt_off, t.lpt_off)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_lpn, lpn)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_lpw, lpw)) != WST_OK) return rc;
-    if ((rc = upload(&plan->d_lpw_off, lpw_off)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_lpt, lpt)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_lpt_off, t.lpt_off)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_lpn, lpn)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_lpw, lpw)) != WST_OK) return rc;
+    if ((rc = up(&plan->d_lpw_off, lpw_off)) != WST_OK) return rc;
 
     DevParams& dp = plan->dp;
     dp.M = g.M; dp.N = g.N; dp.PM = g.PM; dp.PN = g.PN; dp.J = J; dp.L = L;
@@ -1094,12 +1128,29 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
             return fail(WST_ERR_INVALID, "k_o1 at level " + std::to_string(j1) + ": " +
                                              std::to_string(plan->o1_threads[j1]) +
                                              " threads cannot hold the exported half spectrum (8 items each)");
-    WST_HIP_CHECK(plan->ops->set_attrs());
-    if (plan->rb > 0) {
-        WST_HIP_CHECK(wstlaunch::wst_big_common_ops().set_attrs());
-        for (int r = 0; r < plan->nst; ++r) {
-            WST_HIP_CHECK(plan->big_r[r]->set_attrs());
-            WST_HIP_CHECK(plan->big_c[r]->set_attrs());
+    plan->box1_l0.assign(J, -1);
+    for (int j = 0; j < J; ++j) plan->box1_l0[j] = box1_off[static_cast<size_t>(j) * L];
+    if (device) {
+        // every k_o1 / k_o2 the plan launches must be one of the compiled instantiations
+        const std::vector<int> w = describe_chunk(plan.get());
+        for (size_t i = 0; i < w.size(); i += wstdev::kTraceW) {
+            const int kind = w[i] >> 28, fm = (w[i] >> 22) & 63, fn = (w[i] >> 16) & 63, cap = (w[i] >> 4) & 4095;
+            const int sq = (w[i] >> 1) & 1, hg = w[i] & 1;
+            if ((kind == wstdev::kTkO1 && !wstlaunch::compiled_o1(fm, fn, cap, sq)) ||
+                (kind == wstdev::kTkO2 && !wstlaunch::compiled_o2(fm, fn, cap, sq, hg)))
+                return fail(WST_ERR_UNSUPPORTED, std::string(kind == wstdev::kTkO1 ? "k_o1" : "k_o2") + "<" +
+                                                     std::to_string(fm) + ", " + std::to_string(fn) + ", " +
+                                                     std::to_string(cap) + ", " + std::to_string(sq) +
+                                                     (kind == wstdev::kTkO2 ? ", " + std::to_string(hg) : "") +
+                                                     "> is not compiled (wst_compiled.h; tools/variant_cover.py)");
+        }
+        WST_HIP_CHECK(plan->ops->set_attrs());
+        if (plan->rb > 0) {
+            WST_HIP_CHECK(wstlaunch::wst_big_common_ops().set_attrs());
+            for (int r = 0; r < plan->nst; ++r) {
+                WST_HIP_CHECK(plan->big_r[r]->set_attrs());
+                WST_HIP_CHECK(plan->big_c[r]->set_attrs());
+            }
         }
     }
 
@@ -1107,6 +1158,10 @@ int wst_plan_create_ex(int M, int N, int J, int L, int max_order, int pre_pad,
     g_last_error.clear();
     return WST_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 int wst_plan_destroy(wst_plan* plan) {
     free_plan(plan);
@@ -1230,29 +1285,38 @@ struct LaunchTimer {
 // One LDS-resident level j1: k_o1 (S1 + U1 half-spectrum export), then k_o2 (every S2 of j1).
 int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsigned char* base,
                    int64_t chunk, const float2* xhat, float* d_out, int pooled, hipStream_t stream,
-                   LaunchTimer& timer) {
+                   LaunchTimer& timer, int& site) {
     const wst::Geometry& g = plan->g;
     const bool do2 = g.max_order >= 2 && j1 < g.J - 1;
     float2* hexp = do2 ? reinterpret_cast<float2*>(base + plan->ws_h_off[j1] * chunk) : nullptr;
     int rc;
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
-    plan->ops->o1(plan->cap[j1], plan->sq,
-                  Launch{dim3(nimg * g.L), dim3(plan->o1_threads[j1]), plan->o1_lds[j1], stream},
-                  plan->dp, plan->o1_lay[j1], j1, nimg, img0, xhat, hexp, d_out, pooled);
+    LdsLayout lay1 = plan->o1_lay[j1];
+    lay1.tslot = site++;
+    if (!plan->ops->o1(plan->cap[j1], plan->sq,
+                       Launch{dim3(nimg * g.L), dim3(plan->o1_threads[j1]), plan->o1_lds[j1], stream},
+                       plan->dp, lay1, j1, nimg, img0, xhat, hexp, d_out, pooled))
+        return fail(WST_ERR_UNSUPPORTED, "k_o1 variant not compiled (wst_compiled.h)");
     WST_HIP_CHECK(hipGetLastError());
     if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
     if (!do2) return WST_OK;
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
     if (plan->o2_export[j1]) {   // spectrum exported fully transformed: fold from HBM
-        plan->ops->o2(136, plan->sq, 1, Launch{dim3(nimg * g.L * std::max(1, plan->o2x_lay[j1].nsplit)),
-                                        dim3(plan->o2x_threads[j1]), plan->o2x_lds[j1], stream},
-                      plan->dp, plan->o2x_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j1 + 1);
+        LdsLayout lx = plan->o2x_lay[j1];
+        lx.tslot = site++;
+        if (!plan->ops->o2(136, plan->sq, 1, Launch{dim3(nimg * g.L * std::max(1, plan->o2x_lay[j1].nsplit)),
+                                             dim3(plan->o2x_threads[j1]), plan->o2x_lds[j1], stream},
+                           plan->dp, lx, j1, nimg, img0, hexp, d_out, pooled, j1 + 1))
+            return fail(WST_ERR_UNSUPPORTED, "k_o2 variant not compiled (wst_compiled.h)");
         WST_HIP_CHECK(hipGetLastError());
         return timer.end(stream, 1 + g.J + j1);
     }
-    plan->ops->o2(plan->cap[j1], plan->sq, 0,
-                  Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
-                  plan->dp, plan->o2_lay[j1], j1, nimg, img0, hexp, d_out, pooled, j1 + 1);
+    LdsLayout lay2 = plan->o2_lay[j1];
+    lay2.tslot = site++;
+    if (!plan->ops->o2(plan->cap[j1], plan->sq, 0,
+                       Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
+                       plan->dp, lay2, j1, nimg, img0, hexp, d_out, pooled, j1 + 1))
+        return fail(WST_ERR_UNSUPPORTED, "k_o2 variant not compiled (wst_compiled.h)");
     WST_HIP_CHECK(hipGetLastError());
     return timer.end(stream, 1 + g.J + j1);
 }
@@ -1264,7 +1328,7 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
 // o2 at j1.
 int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img0,
                   unsigned char* base, int64_t chunk, float* d_out, int pooled, hipStream_t stream,
-                  LaunchTimer& timer) {
+                  LaunchTimer& timer, int& site) {
     using namespace wstbig;
     const wst::Geometry& g = plan->g;
     const DevParams& dp = plan->dp;
@@ -1292,6 +1356,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         a.L = L;
         a.img0 = img0;
         a.oms = noms;
+        a.tslot = site++;
         return a;
     };
     // column pass over level r: lines of PM >> r points, `ncols` columns
@@ -1305,6 +1370,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         a.img0 = img0;
         a.oms = noms;
         a.g_lds = plan->big_g_lds[r];
+        a.tslot = site++;
         return a;
     };
     auto col_grid = [&](int ncols, int arrays) { return dim3((ncols + kColTile - 1) / kColTile, arrays); };
@@ -1402,10 +1468,14 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
                       part, gnat(j2, 1), nullptr, nullptr, L, j1, -1, j2, L, img0, d_out, pooled);
         }
         const int j2f = plan->hg_j2first[j1];
-        if (j2f < J)
-            plan->ops->o2(136, 1, 1, Launch{dim3(nimg * L * std::max(1, plan->hg_lay[j1].nsplit)),
-                                            dim3(plan->hg_threads[j1]), plan->hg_lds[j1], stream},
-                          dp, plan->hg_lay[j1], j1, nimg, img0, hbig, d_out, pooled, j2f);
+        if (j2f < J) {
+            LdsLayout lh = plan->hg_lay[j1];
+            lh.tslot = site++;
+            if (!plan->ops->o2(136, 1, 1, Launch{dim3(nimg * L * std::max(1, plan->hg_lay[j1].nsplit)),
+                                                 dim3(plan->hg_threads[j1]), plan->hg_lds[j1], stream},
+                               dp, lh, j1, nimg, img0, hbig, d_out, pooled, j2f))
+                return fail(WST_ERR_UNSUPPORTED, "k_o2 variant not compiled (wst_compiled.h)");
+        }
         WST_HIP_CHECK(hipGetLastError());
         if ((rc = timer.end(stream, 1 + J + j1)) != WST_OK) return rc;
     }
@@ -1501,24 +1571,27 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
     for (int64_t c0 = 0; c0 < nbatch; c0 += chunk) {
         const int nimg = static_cast<int>(std::min<int64_t>(chunk, nbatch - c0));
         const long long img0 = static_cast<long long>(c0);
+        int site = 0;   // variant-trace sites, in launch order (describe_chunk)
         if (plan->rb > 0) {
             if ((rc = staged_levels(plan, d_in + c0 * inM * inN, nimg, img0, base, chunk, d_out, pooled,
-                                    stream, timer)) != WST_OK)
+                                    stream, timer, site)) != WST_OK)
                 return rc;
             for (int j1 = plan->rb; j1 < g.J; ++j1)
                 if ((rc = resident_level(plan, j1, nimg, img0, base, chunk, xhat, d_out, pooled, stream,
-                                         timer)) != WST_OK)
+                                         timer, site)) != WST_OK)
                     return rc;
             continue;
         }
         if ((rc = timer.begin(stream)) != WST_OK) return rc;
+        LdsLayout lp = plan->prep_lay;
+        lp.tslot = site++;
         plan->ops->prep(Launch{dim3(nimg), dim3(plan->prep_threads), plan->prep_lds, stream},
-                        plan->dp, plan->prep_lay, d_in + c0 * inM * inN, img0, xhat, d_out, pooled);
+                        plan->dp, lp, d_in + c0 * inM * inN, img0, xhat, d_out, pooled);
         WST_HIP_CHECK(hipGetLastError());
         if ((rc = timer.end(stream, 0)) != WST_OK) return rc;
         for (int j1 = 0; j1 < g.J; ++j1)
             if ((rc = resident_level(plan, j1, nimg, img0, base, chunk, xhat, d_out, pooled, stream,
-                                     timer)) != WST_OK)
+                                     timer, site)) != WST_OK)
                 return rc;
     }
     if (used) WST_HIP_CHECK(hipEventRecord(used->done, stream));   // the buffer is busy until here
@@ -1526,9 +1599,252 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
     return timer.finish();
 }
 
+// ------------------------------------------------------------------------------------------
+// Host mirror of the kernels' run-time dispatch: the trace words (wst_device.h kTraceW) every
+// launch site of one chunk writes, predicted from the plan alone.  Mirrors k_prep / k_o1 / k_o2
+// (wst_device.h) and the staged passes (wst_staged.h); tests check it against the device trace.
+// ------------------------------------------------------------------------------------------
+using namespace wstdev;
+
+bool rc_ok(int k) { return k > 0 && mfma_k_steps(k) <= 18; }
+int lp_form(bool sq, bool wide, int k) { return sq ? kLpTap : wide ? (rc_ok(k) ? kLpMfmaRc : kLpMfma) : kLpPlain; }
+
+struct Describe {
+    const wst_plan* plan;
+    std::vector<int> w;
+    int* site() {
+        w.resize(w.size() + kTraceW, 0);
+        return w.data() + w.size() - kTraceW;
+    }
+};
+
+void describe_prep(Describe& d) {
+    const wst_plan* pl = d.plan;
+    const wst::Geometry& g = pl->g;
+    const int FM = pl->fam_m, FN = pl->fam_n;
+    int pc = 0;
+    if (FM == FN && FM > 0)
+        for (int mc = 0; mc < 8 && !pc; ++mc) {
+            const int PC = FM << mc;
+            if (PC > 48 && PC <= 136 && g.PM == PC && g.PN == PC) pc = PC;
+        }
+    const bool wide = g.oM > kLpOM || g.oN > kLpOM;
+    int* t = d.site();
+    t[0] = tr_kernel(kTkPrep, FM, FN, 0, 0, 0);
+    t[1] = tr_prep(pc, wide ? (rc_ok(pc) ? kLpMfmaRc : kLpMfma) : kLpPlain);
+}
+
+void describe_o1(Describe& d, int j1) {
+    const wst_plan* pl = d.plan;
+    const wst::Geometry& g = pl->g;
+    const int FM = pl->fam_m, FN = pl->fam_n, MAXN = pl->cap[j1];
+    const int SQ = (FM == FN && FM > 0 && pl->sq) ? 1 : 0;
+    const LdsLayout& lay = pl->o1_lay[j1];
+    int oc = 0, n1t = 0;
+    if (SQ && MAXN == 136 && g.oM == 4 && g.oN == 4 && lay.oms == 4) {
+        oc = 4;
+    } else if (!SQ && FM == FN && FM > 0 && g.PM == g.PN) {
+        for (int mc = 0; mc < 8 && !n1t; ++mc) {
+            const int n1x = FM << mc;
+            if (n1x <= MAXN && n1x > prev_cap(MAXN) && (g.PM >> j1) == n1x) n1t = n1x;
+        }
+    }
+    const int n1c = n1t ? n1t : SQ ? unique_level(FM, MAXN) : 0;
+    const bool fuse1 = SQ && n1c >= kFuse1Min && wstfft::split_n2(n1c) > 1;
+    const bool fused1 = fuse1 && j1 == 0;
+    const bool do2 = g.max_order >= 2 && j1 < g.J - 1;
+    const int s1 = 1 << j1;
+    const bool box1 = pl->box1_l0[j1] >= 0 && s1 >= pl->dp.box1_min_s;
+    const int f1 = fused1 ? 0 : s1 == 1 ? 1 : s1 == 2 ? 2 : box1 ? 3 : s1 == 4 ? 4 : 5;
+    const bool wide = g.oM > kLpOM || g.oN > kLpOM;
+    int* t = d.site();
+    t[0] = tr_kernel(kTkO1, FM, FN, MAXN, SQ, 0);
+    t[1] = tr_o1(oc, n1c, fused1 ? 1 : 0, lp_form(SQ, wide, n1c), do2 ? 1 : 0, lay.export_full, f1);
+}
+
+void describe_o2(Describe& d, int j1, const LdsLayout& lay, int MAXN, int sq, int HG, int j2first) {
+    const wst_plan* pl = d.plan;
+    const wst::Geometry& g = pl->g;
+    const int FM = pl->fam_m, FN = pl->fam_n, J = g.J, L = g.L, PM = g.PM, PN = g.PN;
+    const bool square_fam = FM == FN && FM > 0;
+    const int SQ = (square_fam && sq) ? 1 : 0;
+    if (!square_fam) HG = 0;   // FamilyOps::o2 of a non-square pair has no HG kernels
+    int oc = 0, lc = 0;
+    if (SQ && g.oM == 4 && g.oN == 4 && lay.oms == 4) {
+        oc = 4;
+        lc = (unique_level(FM, MAXN) > 0 && L == 8) ? 8 : 0;
+    } else if (!SQ && HG && square_fam && L == 8) {
+        lc = 8;
+    }
+    const int n1c = (SQ && !HG) ? unique_level(FM, MAXN) : 0;
+    const int spec = HG ? 0 : (n1c > 0 && wstfft::split_n2(n1c) > 1) ? 1 : 2;
+    const bool wide = g.oM > kLpOM || g.oN > kLpOM;
+    int* t = d.site();
+    auto level = [&](int j2, int pb, int sc, int nc) {
+        const int n1f = (SQ && nc > 0 && sc > 0) ? nc * sc : 0;
+        const bool fuse = n1f > 0 && sc == 2 && n1f / 2 >= kFuseMin && wstfft::split_n2(n1f / 2) > 1;
+        const int s2 = 1 << (j2 - j1);
+        const int fk = fuse ? kFdFused : (n1f > 0 && sc == 2) ? kFdTileS2
+                     : (n1f > 0 && (sc == 4 || sc == 8)) ? kFdTileList : s2 == 2 ? kFdDenseS2 : kFdBox;
+        if (2 + (j2 - j1 - 1) < kTraceW) t[2 + (j2 - j1 - 1)] = tr_level(j2, pb, sc, nc, fk, lp_form(SQ, wide, nc), s2);
+    };
+    int branch = 7;
+    if (n1c > 0) {
+        branch = 1;
+        for (int k = 1; k < 8; ++k) {
+            const int nn2 = n1c >> k;
+            if ((nn2 << k) == n1c && nn2 >= 1 && j1 + k < J && j1 + k >= j2first)
+                level(j1 + k, lc == 0 ? 0 : (k == 1 && MAXN > kWholeFirstCap) ? 2 : lc, 1 << k, nn2);
+        }
+    } else if (SQ && HG && unique_level(FM, MAXN) > 0) {
+        const int n2c = unique_level(FM, MAXN);
+        if (j2first == j1 + 1 && (PM >> j1) == n2c && PM == PN) {
+            branch = 2;
+            for (int k = 1; k < 8; ++k) {
+                const int nn2 = n2c >> k;
+                if ((nn2 << k) == n2c && nn2 >= 1 && j1 + k < J)
+                    level(j1 + k, lc == 0 ? 0 : k == 1 ? 2 : lc, 1 << k, nn2);
+            }
+        } else if ((PM >> j2first) == n2c) {
+            branch = 3;
+            for (int k = 0; k < 8; ++k) {
+                const int nn2 = n2c >> k;
+                if ((nn2 << k) == n2c && nn2 >= 1 && j2first + k < J) level(j2first + k, 0, 0, 0);
+            }
+        } else {
+            branch = 4;
+            for (int j2 = j2first; j2 < J; ++j2) level(j2, 0, 0, 0);
+        }
+    } else if (!SQ && HG && square_fam) {
+        int n1x = 0;
+        if (PM == PN && j2first == j1 + 1)
+            for (int mc = 0; mc < 8 && !n1x; ++mc) {
+                const int c = FM << mc;
+                if (c <= MAXN && c > prev_cap(MAXN) && (PM >> j1) == c) n1x = c;
+            }
+        if (n1x) {
+            branch = 5;
+            for (int k = 1; k < 8; ++k) {
+                const int nn2 = n1x >> k;
+                if ((nn2 << k) == n1x && nn2 >= 1 && j1 + k < J) level(j1 + k, lc == 0 ? 0 : k == 1 ? 2 : lc, 0, nn2);
+            }
+        } else {
+            branch = 6;
+            for (int j2 = j2first; j2 < J; ++j2) level(j2, 0, 0, 0);
+        }
+    } else {
+        for (int j2 = j2first; j2 < J; ++j2) level(j2, 0, 0, 0);
+    }
+    (void)PN;
+    t[0] = tr_kernel(kTkO2, FM, FN, MAXN, SQ, HG);
+    t[1] = tr_o2(oc, lc, n1c, spec, branch);
+}
+
+void describe_big(Describe& d, bool rows, int n, bool inv, int body) {
+    int* t = d.site();
+    t[0] = tr_kernel(rows ? kTkBigRows : kTkBigCols, 0, 0, n, 0, inv ? 1 : 0);
+    t[1] = body;
+}
+
+// One chunk's launch sites in forward_impl's order (staged_levels / resident_level).
+std::vector<int> describe_chunk(const wst_plan* pl) {
+    Describe d{pl, {}};
+    const wst::Geometry& g = pl->g;
+    const int J = g.J, L = g.L;
+    const int wide_maps = g.oM > 8 ? 1 : 0;
+    auto resident = [&](int j1) {
+        describe_o1(d, j1);
+        if (!(g.max_order >= 2 && j1 < J - 1)) return;
+        if (pl->o2_export[j1]) describe_o2(d, j1, pl->o2x_lay[j1], 136, pl->sq, 1, j1 + 1);
+        else describe_o2(d, j1, pl->o2_lay[j1], pl->cap[j1], pl->sq, 0, j1 + 1);
+    };
+    if (pl->rb > 0) {
+        using namespace wstbig;
+        describe_big(d, true, pl->big_r[0]->n, false, tr_big(kRowPad, 0, 0, 0, 0, 0, 0));
+        describe_big(d, false, pl->big_c[0]->n, false, tr_big(kColStore, 0, 0, 0, 0, 0, 0));
+        for (int j1 = 0; j1 < pl->rb; ++j1) {
+            const bool do2 = g.max_order >= 2 && j1 < J - 1;
+            describe_big(d, true, pl->big_r[j1]->n, true, tr_big(kRowFold1, 0, j1 == 0 ? 1 : 2, 0, 0, 0, 0));
+            describe_big(d, false, pl->big_c[j1]->n, true,
+                         tr_big(kColModLp, 0, 0, 0, wide_maps, pl->big_g_lds[j1], do2 ? 1 : 0));
+            if (!do2) continue;
+            describe_big(d, true, pl->big_r[j1]->n, false, tr_big(kRowReal2, 0, 0, 0, 0, 0, 0));
+            describe_big(d, false, pl->big_c[j1]->n, false, tr_big(kColStore, 0, 0, 0, 0, 0, 0));
+            for (int j2 = j1 + 1; j2 < pl->nst; ++j2) {
+                const int m1 = g.PM >> j1, m2 = g.PM >> j2;
+                const bool fold_all = m1 == 2 * m2 && pl->fold_all_rows[j2] > 0;
+                const bool box = !fold_all && (1 << (j2 - j1)) >= 4;
+                for (int l1 = 0; l1 < L; ++l1) {
+                    describe_big(d, true, pl->big_r[j2]->n, true, tr_big(kRowFold2, fold_all ? 1 : 0, 0, box ? 1 : 0, 0, 0, 0));
+                    describe_big(d, false, pl->big_c[j2]->n, true,
+                                 tr_big(kColModLp, 0, 0, 0, wide_maps, pl->big_g_lds[j2], 0));
+                }
+            }
+            const int j2f = pl->hg_j2first[j1];
+            if (j2f < J) describe_o2(d, j1, pl->hg_lay[j1], 136, 1, 1, j2f);
+        }
+        for (int j1 = pl->rb; j1 < J; ++j1) resident(j1);
+    } else {
+        describe_prep(d);
+        for (int j1 = 0; j1 < J; ++j1) resident(j1);
+    }
+    return d.w;
+}
+
+int copy_words(const std::vector<int>& w, int32_t* out, int64_t max_words, int64_t* nwords) {
+    if (!nwords) return fail(WST_ERR_INVALID, "nwords is NULL");
+    *nwords = static_cast<int64_t>(w.size());
+    if (out) {
+        if (max_words < static_cast<int64_t>(w.size())) return fail(WST_ERR_INVALID, "output buffer too small");
+        for (size_t i = 0; i < w.size(); ++i) out[i] = w[i];
+    }
+    return WST_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int wst_plan_variants(const wst_plan* plan, int32_t* out, int64_t max_words, int64_t* nwords) {
+    if (!plan) return fail(WST_ERR_INVALID, "plan is NULL");
+    return copy_words(describe_chunk(plan), out, max_words, nwords);
+}
+
+int wst_describe_variants(int M, int N, int J, int L, int max_order, int32_t* out, int64_t max_words,
+                          int64_t* nwords) {
+    wst_plan* p = nullptr;
+    const int rc = create_plan(M, N, J, L, max_order, 0, nullptr, false, &p);
+    if (rc != WST_OK) return rc;
+    const std::vector<int> w = describe_chunk(p);
+    free_plan(p);
+    return copy_words(w, out, max_words, nwords);
+}
+
+int wst_plan_trace(wst_plan* plan, int enable) {
+    if (!plan) return fail(WST_ERR_INVALID, "plan is NULL");
+    if (plan->host_only) return fail(WST_ERR_INVALID, "host-only plan");
+    if (!enable) {
+        plan->dp.vtrace = nullptr;
+        return WST_OK;
+    }
+    const size_t bytes = static_cast<size_t>(kTraceSites) * kTraceW * sizeof(int);
+    if (!plan->d_trace) WST_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&plan->d_trace), bytes));
+    WST_HIP_CHECK(hipMemset(plan->d_trace, 0, bytes));
+    plan->dp.vtrace = plan->d_trace;
+    return WST_OK;
+}
+
+int wst_plan_read_trace(const wst_plan* plan, int32_t* out, int64_t max_words, int64_t* nwords) {
+    if (!plan || !out || !nwords) return fail(WST_ERR_INVALID, "plan/out/nwords is NULL");
+    if (!plan->d_trace) return fail(WST_ERR_INVALID, "tracing was never enabled (wst_plan_trace)");
+    const int64_t n = std::min<int64_t>(static_cast<int64_t>(describe_chunk(plan).size()),
+                                        static_cast<int64_t>(kTraceSites) * kTraceW);
+    if (max_words < n) return fail(WST_ERR_INVALID, "output buffer too small");
+    WST_HIP_CHECK(hipDeviceSynchronize());
+    WST_HIP_CHECK(hipMemcpy(out, plan->d_trace, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToHost));
+    *nwords = n;
+    return WST_OK;
+}
 
 int wst_forward(const wst_plan* plan, const float* d_in, int64_t nbatch, float* d_out, int pooled,
                 void* d_workspace, size_t workspace_bytes, void* stream) {

@@ -25,11 +25,12 @@ struct FamilyOps {
     hipError_t (*set_attrs)();
     void (*prep)(const Launch&, const DevParams&, const LdsLayout&, const float* in, long long img0,
                  float2* xhat, float* out, int pooled);
-    // cap: size class (12/24/48/136); sq: square fused variant (only for fm == fn > 0)
-    void (*o1)(int cap, int sq, const Launch&, const DevParams&, const LdsLayout&, int j1, int nimg,
+    // cap: size class (12/24/48/136); sq: square fused variant (only for fm == fn > 0).
+    // false: the selected instantiation is not compiled (wst_compiled.h), nothing was launched
+    bool (*o1)(int cap, int sq, const Launch&, const DevParams&, const LdsLayout&, int j1, int nimg,
                long long img0, const float2* xhat, float2* hexp, float* out, int pooled);
     // hg: spectrum of a big level read from HBM (square families, cap 136), paths from j2first
-    void (*o2)(int cap, int sq, int hg, const Launch&, const DevParams&, const LdsLayout&, int j1,
+    bool (*o2)(int cap, int sq, int hg, const Launch&, const DevParams&, const LdsLayout&, int j1,
                int nimg, long long img0, const float2* hexp, float* out, int pooled, int j2first);
 };
 
