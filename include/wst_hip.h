@@ -132,7 +132,8 @@ int wst_forward(const wst_plan* plan, const float* d_in, int64_t nbatch, float* 
 
 /*
  * wst_forward + per-kernel timing with HIP events recorded on `stream` around every launch
- * (synchronises the stream before returning).  kernel_ms[0] = sum of k_prep launches,
+ * (the launches stay back to back: the events are read once the last one has completed;
+ * synchronises before returning).  kernel_ms[0] = sum of k_prep launches,
  * kernel_ms[1 + j1] = sum of the k_o1 launches at scale j1 (0 <= j1 < J), kernel_ms[1 + J + j1]
  * = sum of the k_o2 launches at scale j1 (0 <= j1 < J - 1; slot 2J stays 0); n_kernel_ms is the
  * capacity of kernel_ms (slots beyond it are not reported).  Used by bench.py for the
@@ -185,8 +186,11 @@ int wst_host_filter_ex(int M, int N, int J, int L, int kind, int j, int l, int r
  * Line (b, l) element e lives at complex index b*bs + l*ls + e*es; n is the line length,
  * `threads` the workgroup size whose round structure is emulated; inverse is unnormalised.
  * mode 0: natural -> natural; 1: natural -> digit-reversed (in place); 2: digit-reversed ->
- * natural (in place).  `perm` (nullable, n ints) receives the digit-reversal map (physical
- * position -> logical index).  Sizes without a compiled FFT run the generic DFT (mode 0 only).
+ * natural (in place); 3: mode 2 with the first stage reading a copy of the input (k_o2's
+ * fft_lines_rd_from); 4: mode 1 with the fused order-2 rows' split (N = (N / N2O) x N2O,
+ * wst_device.h fused_row_n2; n = 48 only).  `perm` (nullable, n ints) receives the
+ * digit-reversal map (physical position -> logical index) of the transform that ran.  Sizes
+ * without a compiled FFT run the generic DFT (mode 0 only).
  */
 int wst_host_fft_lines(int n, int inverse, int mode, float* data, int nb, int bs, int nl, int ls,
                        int es, int threads, int* perm);

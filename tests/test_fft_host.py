@@ -88,21 +88,28 @@ def test_rd_from_global_equals_inplace(n, inverse):
 
 
 @pytest.mark.parametrize("nn,rs", [(48, 8)])
-def test_fused_row_split_column_remap(nn, rs):
+@pytest.mark.parametrize("inverse", [False, True])
+def test_fused_row_split_column_remap(nn, rs, inverse):
     """The S2 pass of the 48^2 order-2 paths (csrc/wst_device.h cols_modlp RS) walks the tap matrix
     GN in the split_n2 digit-reversed order and reads each logical column's partial from its place
     in the rows' order (split (nn / rs) x rs, fused_row_n2): the remap must land every GN row on the
-    physical column that holds the same logical column.  The library's own digit-reversal map
-    (mode 1 perm) fixes the split_n2 side."""
-    x = np.zeros(nn, np.complex64)
-    perm_default = _lib.host_fft_lines(x, nn, True, 1, 0, 1, nn, 1, 64, mode=1)
+    physical column that holds the same logical column.  Both sides come from the library: the
+    split_n2 order from mode 1, the rows' order from mode 4 (the transform with the fused rows'
+    split, LineFFT<48, true, 8>), whose output is also checked to be that permutation of the DFT."""
+    rng = np.random.default_rng(5)
+    x = (rng.standard_normal(nn) + 1j * rng.standard_normal(nn)).astype(np.complex64)
+    perm_default = _lib.host_fft_lines(x.copy(), nn, inverse, 1, 0, 1, nn, 1, 64, mode=1)
+    y = x.copy()
+    perm_rows = _lib.host_fft_lines(y, nn, inverse, 1, 0, 1, nn, 1, 64, mode=4)
+    ref = np.fft.ifft(x.astype(np.complex128)) * nn if inverse else np.fft.fft(x.astype(np.complex128))
+    assert np.abs(y - ref[perm_rows]).max() / np.abs(ref).max() < 3e-6 * np.log2(nn)
     n2d = next(d for d in range(int(nn ** 0.5), 0, -1) if nn % d == 0)
     n1d, n1r = nn // n2d, nn // rs
     seen = set()
     for q in range(nn):
         lg = q // n2d + n1d * (q % n2d)
         assert lg == perm_default[q]
-        qr = rs * (lg % n1r) + lg // n1r
-        assert qr // rs + n1r * (qr % rs) == lg        # rows' digit-reversed order
+        qr = rs * (lg % n1r) + lg // n1r               # the kernel's remap (cols_modlp RS)
+        assert perm_rows[qr] == lg                     # the rows' transform holds lg there
         seen.add(qr)
     assert seen == set(range(nn))

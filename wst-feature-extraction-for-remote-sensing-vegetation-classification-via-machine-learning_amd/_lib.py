@@ -156,14 +156,17 @@ def load() -> ctypes.CDLL:
         lib.wst_host_fft_lines.restype = c_int
         lib.wst_host_fft_lines.argtypes = [c_int, c_int, c_int, c_vp] + [c_int] * 6 + [c_vp]
         i64p = ctypes.POINTER(c_i64)
-        lib.wst_plan_variants.restype = c_int
-        lib.wst_plan_variants.argtypes = [c_vp, c_vp, c_i64, i64p]
-        lib.wst_describe_variants.restype = c_int
-        lib.wst_describe_variants.argtypes = [c_int] * 5 + [c_vp, c_i64, i64p]
-        lib.wst_plan_trace.restype = c_int
-        lib.wst_plan_trace.argtypes = [c_vp, c_int]
-        lib.wst_plan_read_trace.restype = c_int
-        lib.wst_plan_read_trace.argtypes = [c_vp, c_vp, c_i64, i64p]
+        # (an older A/B build chosen by use_library may lack the introspection entry points;
+        # tests/test_abi.py checks the product library exports all of EXPORTS)
+        if hasattr(lib, "wst_plan_variants"):
+            lib.wst_plan_variants.restype = c_int
+            lib.wst_plan_variants.argtypes = [c_vp, c_vp, c_i64, i64p]
+            lib.wst_describe_variants.restype = c_int
+            lib.wst_describe_variants.argtypes = [c_int] * 5 + [c_vp, c_i64, i64p]
+            lib.wst_plan_trace.restype = c_int
+            lib.wst_plan_trace.argtypes = [c_vp, c_int]
+            lib.wst_plan_read_trace.restype = c_int
+            lib.wst_plan_read_trace.argtypes = [c_vp, c_vp, c_i64, i64p]
         v = lib.wst_abi_version()
         if v != ABI_VERSION:
             raise RuntimeError(f"{LIB_NAME} ABI version {v} != expected {ABI_VERSION}; rebuild it")
@@ -219,7 +222,8 @@ def default_convention() -> Convention:
 def host_fft_lines(data: np.ndarray, n, inverse, nb, bs, nl, ls, es, threads=256, mode=0):
     """In-place host emulation of the device line FFT on a complex64 buffer (test hook).
     mode 0 natural->natural, 1 natural->digit-reversed, 2 digit-reversed->natural, 3 = mode 2 with
-    the first stage reading a copy of the input (k_o2's fft_lines_rd_from; two-stage sizes).
+    the first stage reading a copy of the input (k_o2's fft_lines_rd_from; two-stage sizes), 4 = mode 1
+    with the fused order-2 rows' split (n = 48: LineFFT<48, INV, 8>).
     Returns the digit-reversal map (physical position -> logical index)."""
     assert data.dtype == np.complex64 and data.flags.c_contiguous
     perm = np.zeros(n, np.int32)

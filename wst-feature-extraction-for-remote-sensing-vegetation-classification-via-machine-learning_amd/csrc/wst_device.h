@@ -177,6 +177,9 @@ constexpr int tr_big(int mode, int fold_all, int fold1, int box, int wide, int g
     return mode | (fold_all << 2) | (fold1 << 3) | (box << 5) | (wide << 6) | (glds << 7) | (ustore << 8);
 }
 __device__ __forceinline__ void trace_word(const DevParams& p, int tslot, int k, int v) {
+#ifdef WST_NO_TRACE   // A/B builds only (tools/variant.sh)
+    return;
+#endif
     if (p.vtrace && tslot >= 0 && tslot < kTraceSites && threadIdx.x == 0 && blockIdx.x == 0 &&
         blockIdx.y == 0)
         p.vtrace[tslot * kTraceW + k] = v;
@@ -689,7 +692,7 @@ __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int 
 // wave's column tile (nt = wave % nnt) for all of its (b, row-tile) tasks, step 2's operands are
 // issued at entry, behind step 1 -- instead of once per 8 K steps of every task (the L2 latency of
 // the tap loads, not the matrix pipe, bounded the phase).  Same operand order, K parts and results
-// as lds_lowpass_mfma.  Needs nw % nnt == 0.  Ends with a barrier.
+// as lds_lowpass_mfma.  Any wave count (see step 1).  Ends with a barrier.
 constexpr int mfma_k_steps(int k) {
     return 16 * (k / 64) + 4 * ((k % 64) / 16) + ((k % 16) + 3) / 4;
 }
@@ -748,12 +751,13 @@ __device__ __forceinline__ void lds_lowpass_mfma_rc(float2* U, int nb, int bs, i
         at2 = (t2_0 % (nat * nnt)) / nnt;
         load_ops(GM, nat, at2, g2);
     }
-    // 1. T = U GN
-    {
+    // 1. T = U GN: with nw >= nnt every wave keeps one column tile (waves w and w + nnt share
+    //    it, splitting its row tiles); with fewer waves than tiles a wave takes tiles w, w + nw, ...
+    const bool wide_wg = nw >= nnt;
+    for (int nt = wide_wg ? wave % nnt : wave; nt < nnt; nt += wide_wg ? nnt : nw) {
         float g[KS];
-        const int nt = wave % nnt;
         load_ops(GN, nnt, nt, g);
-        for (int tk = wave / nnt; tk < nb * NMT; tk += nw / nnt) {
+        for (int tk = wide_wg ? wave / nnt : 0; tk < nb * NMT; tk += wide_wg ? nw / nnt : 1) {
             const int b = tk / NMT, mt = tk - b * NMT;
             float2* Ub = U + b * bs;
             const int p = mt * 16 + li;

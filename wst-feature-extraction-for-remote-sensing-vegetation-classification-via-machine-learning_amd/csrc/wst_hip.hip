@@ -595,16 +595,34 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
     // which some bin of the tile meets a bin where either filter of the pair exceeds kBoxThreshold
     // of its maximum (every tap the box fold keeps at that bin), direct (b < s/2) then mirrored,
     // each padded to groups of four with dummy taps that read the zero block appended to psi2.
+    // square variant (bounded FFT sizes + fused order-2 low-pass): square plane of a compiled
+    // family, oM <= kLpOM and every order-2 level's column units hold ceil(oM / 2) slots
+    plan->sq = (plan->fam_m > 0 && plan->fam_m == plan->fam_n && g.PM == g.PN &&
+                g.oM <= wstdev::kLpOM) ? 1 : 0;
+    for (int j2 = 1; j2 < J; ++j2)
+        if (rows_per_unit(g.PM >> j2) < (g.oM + 1) / 2) plan->sq = 0;
+    if (const char* e = diag_env("WST_SQ")) plan->sq = plan->sq && std::atoi(e) != 0;
+
+    // Only the levels that run them get lists: LDS-resident levels of SQ plans whose size class
+    // holds one size of the family (the kernels' compile-time level N1C, k_o2 branch N1C).
     std::vector<int> taph, taps;
     std::vector<int> taph_off(static_cast<size_t>(J) * J, 0);
     size_t psi2_zero = 0;   // float2 index of the zero block (dummy taps)
-    if (max_order >= 2 && g.PM == g.PN && device) {
+    const auto tile_level = [&](int j2, int r) {
+        const int S = 1 << (j2 - r), N1 = g.PM >> r;
+        return S >= 4 && S <= 8 && plan->sq && N1 <= wstbig::kBigMinN &&
+               wstdev::unique_level(plan->fam_m, cap_for(N1)) == N1;
+    };
+    bool any_tiles = false;
+    for (int j2 = 1; j2 < J; ++j2)
+        for (int r = 0; r < j2 && r < wst::psi_levels(j2, J); ++r) any_tiles = any_tiles || tile_level(j2, r);
+    if (max_order >= 2 && g.PM == g.PN && device && any_tiles) {
         psi2_zero = psi2.size();
         psi2.resize(psi2.size() + static_cast<size_t>(g.PM) * g.PM / 2 + 64, make_float2(0.f, 0.f));
         for (int j2 = 1; j2 < J; ++j2)
             for (int r = 0; r < j2 && r < wst::psi_levels(j2, J); ++r) {
                 const int S = 1 << (j2 - r), N1 = g.PM >> r, N2 = g.PM >> j2, HLD = N1 / 2 + 1;
-                if (S < 4 || S > 8) continue;
+                if (!tile_level(j2, r)) continue;
                 const int items = N2 * N2, nt = (items + 63) / 64;
                 taph_off[static_cast<size_t>(j2) * J + r] = static_cast<int>(taph.size() / 4);
                 for (int q = 0; q < nq; ++q) {
@@ -845,14 +863,6 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
     if (const char* e = diag_env("WST_BOX1_MIN_S")) dp.box1_min_s = std::atoi(e);
     dp.lpt = plan->d_lpt; dp.lpt_off = plan->d_lpt_off;
     dp.lpw = plan->d_lpw; dp.lpw_off = plan->d_lpw_off; dp.oMp = oMp; dp.oNp = oNp;
-    // square variant (bounded FFT sizes + fused order-2 low-pass): square plane of a compiled
-    // family, oM <= kLpOM and every order-2 level's column units hold ceil(oM / 2) slots
-    plan->sq = (plan->fam_m > 0 && plan->fam_m == plan->fam_n && g.PM == g.PN &&
-                g.oM <= wstdev::kLpOM) ? 1 : 0;
-    for (int j2 = 1; j2 < J; ++j2)
-        if (rows_per_unit(g.PM >> j2) < (g.oM + 1) / 2) plan->sq = 0;
-    if (const char* e = diag_env("WST_SQ")) plan->sq = plan->sq && std::atoi(e) != 0;
-
     // --- LDS layouts ---
     const size_t omn = static_cast<size_t>(g.oM) * g.oN;
     const auto too_big = [&](const char* what, int j) {
@@ -1912,8 +1922,9 @@ int wst_host_filter_ex(int M, int N, int J, int L, int kind, int j, int l, int r
 
 int wst_host_fft_lines(int n, int inverse, int mode, float* data, int nb, int bs, int nl, int ls,
                        int es, int threads, int* perm) {
-    if (!data || n < 1 || nb < 1 || nl < 1 || threads < 1 || mode < 0 || mode > 3)
+    if (!data || n < 1 || nb < 1 || nl < 1 || threads < 1 || mode < 0 || mode > 4)
         return fail(WST_ERR_INVALID, "bad arguments");
+    bool perm_done = false;
     std::vector<float2> tw(static_cast<size_t>(n));
     for (int k = 0; k < n; ++k) {
         const double a = 2.0 * 3.14159265358979323846 * k / n;
@@ -1932,6 +1943,23 @@ int wst_host_fft_lines(int n, int inverse, int mode, float* data, int nb, int bs
         if (mode == 0) {                                                                   \
             if (inverse) wstfft::fft_lines_host<NN, true>(base, g, tw.data(), threads);    \
             else wstfft::fft_lines_host<NN, false>(base, g, tw.data(), threads);           \
+        } else if (mode == 4) {                                                            \
+            /* F_DR with the fused order-2 rows' split (wstdev::fused_row_n2) */              \
+            constexpr int N2O = wstdev::fused_row_n2(NN);                                      \
+            if constexpr (N2O > 0) {                                                           \
+                using FO = wstfft::LineFFT<NN, true, N2O>;                                     \
+                using FF = wstfft::LineFFT<NN, false, N2O>;                                    \
+                wstfft::EpiIdentity id4;                                                       \
+                for (int u = 0; u < g.nlines() * FO::N2; ++u)                                  \
+                    inverse ? FO::stageA_unit(base, g, tw.data(), u) : FF::stageA_unit(base, g, tw.data(), u); \
+                for (int u = 0; u < g.nlines() * FO::N1; ++u)                                  \
+                    inverse ? FO::stageB_inplace(base, g, u, id4) : FF::stageB_inplace(base, g, u, id4); \
+                if (perm)                                                                      \
+                    for (int pos = 0; pos < NN; ++pos) perm[pos] = FO::dr_logical(pos);        \
+                perm_done = true;                                                              \
+            } else {                                                                           \
+                return fail(WST_ERR_UNSUPPORTED, "mode 4 needs a fused-row size (48)");        \
+            }                                                                                  \
         } else if (mode == 3) {                                                            \
             if (wstfft::LineFFT<NN, false>::N2 == 1)                                       \
                 return fail(WST_ERR_UNSUPPORTED, "mode 3 needs a two-stage size");         \
@@ -1949,7 +1977,7 @@ int wst_host_fft_lines(int n, int inverse, int mode, float* data, int nb, int bs
         default:
             break;
     }
-    if (perm)
+    if (perm && !perm_done)
         for (int pos = 0; pos < n; ++pos) perm[pos] = compiled ? wstfft::dr_logical_host(n, pos) : pos;
     if (compiled) return WST_OK;
     if (mode != 0) return fail(WST_ERR_UNSUPPORTED, "in-place modes need a compiled FFT size");
