@@ -31,7 +31,7 @@
 // Phase-skipping ablation mask (DevParams::dbg_skip): compiled in only for diagnostic builds
 // (-DWST_DIAG); production kernels see a constant 0 and carry no skip branches.
 #ifdef WST_DIAG
-#define WST_DBG_MASK(p) ((p).dbg_skip)
+#define WST_DBG_MASK(p) ((p).flags & 0x3fffffff)
 #else
 #define WST_DBG_MASK(p) 0
 #endif
@@ -42,7 +42,10 @@ namespace wstdev {
 // (compile-time square levels); elements whose fold loads one fused unit keeps in flight
 constexpr int kFuseMin = 48;
 constexpr int kFuse1Min = 48;
-constexpr int kFuseGroup = 4;
+#ifndef WST_FUSE_GROUP   // A/B builds (tools/variant.sh -DWST_FUSE_GROUP=n)
+#define WST_FUSE_GROUP 4
+#endif
+constexpr int kFuseGroup = WST_FUSE_GROUP;
 // SQ k_o2 of size classes up to this cap: B holds all L paths of the first order-2 level too (host:
 // bcap), so that level runs as one batch instead of L / 2 filter-pair batches (c2 k_o2 j1 = 2
 // 0.160 -> 0.122 ms per step; at the 48 class, j1 = 1, 0.509 -> 0.604: the larger B cuts the
@@ -62,7 +65,8 @@ constexpr int kMaxO = 8;  // outputs per thread per generic-DFT chunk
 struct DevParams {
     int M, N, PM, PN, J, L, max_order, pre_pad, K;
     int mM, mN, oM, oN, padTop, padLeft;
-    int dbg_skip;                 // timing-ablation mask (env WST_DEBUG_SKIP, WST_DIAG builds only)
+    int flags;                    // bits 0-29: timing-ablation mask (env WST_DEBUG_SKIP, WST_DIAG
+                                  // builds only); kFlagTrace: variant trace on (wst_plan_trace)
     const float* psi;             // concatenated psi Fourier levels (fp32)
     const long long* psi_off;     // [(j*L + l)*J + r]
     const float* lp;              // spatial low-pass taps per level, each stored twice
@@ -96,8 +100,10 @@ struct DevParams {
     const int4* taph;
     const int* taph_off;
     const int2* taps;
-    int* vtrace;                  // variant trace (wst_plan_trace, tests); nullptr: off
 };
+// DevParams::flags bit: the variant trace is on; its words follow the o2_base table (J L ints).
+// (No separate pointer: one more kernel argument made the headline k_o2 spill SGPRs, +3 %.)
+constexpr int kFlagTrace = 1 << 30;
 
 // Per-launch LDS layout (byte offsets) and the table slices copied into LDS.
 struct LdsLayout {
@@ -120,12 +126,12 @@ struct LdsLayout {
     int hext;               // resident levels: an item's half spectrum in the workspace holds
                             // nM1 + 1 rows (row nM1 = row 0 for the tile folds' mirrored taps;
                             // written by an exporting k_o1, formed in LDS by k_o2 otherwise)
-    int tslot;              // variant-trace site of this launch (DevParams::vtrace)
+    int tslot;              // variant-trace site of this launch (kFlagTrace)
 };
 
 // ------------------------------------------------------------------------------------------
 // Variant trace (tests: wst_plan_trace / wst_describe_variants, include/wst_hip.h).  With
-// DevParams::vtrace set, workgroup 0 of every traced launch writes kTraceW words at its site
+// kFlagTrace set in DevParams::flags, workgroup 0 of every traced launch writes kTraceW words at its site
 // (LdsLayout::tslot / BigArgs::tslot): word 0 the kernel instantiation, word 1 the body it
 // dispatched to at run time, words 2.. (k_o2) the branch of each order-2 level it ran (index
 // j2 - j1 - 1).  The host mirror in wst_hip.hip (describe_chunk) predicts the same words from the
@@ -176,13 +182,18 @@ constexpr int tr_level(int j2, int pb, int sc, int nc, int fold, int lp, int s2)
 constexpr int tr_big(int mode, int fold_all, int fold1, int box, int wide, int glds, int ustore) {
     return mode | (fold_all << 2) | (fold1 << 3) | (box << 5) | (wide << 6) | (glds << 7) | (ustore << 8);
 }
-__device__ __forceinline__ void trace_word(const DevParams& p, int tslot, int k, int v) {
+// The writer of a site: lane 0 of workgroup 0, only while tracing.  Callers wrap the whole
+// word computation in `if (tracing(p, tslot))` so a production launch (kFlagTrace clear) skips
+// it with one uniform branch and the hot code around it is laid out as without it.
+__device__ __forceinline__ bool tracing(const DevParams& p, int tslot) {
 #ifdef WST_NO_TRACE   // A/B builds only (tools/variant.sh)
-    return;
+    return false;
 #endif
-    if (p.vtrace && tslot >= 0 && tslot < kTraceSites && threadIdx.x == 0 && blockIdx.x == 0 &&
-        blockIdx.y == 0)
-        p.vtrace[tslot * kTraceW + k] = v;
+    return (p.flags & kFlagTrace) && tslot >= 0 && tslot < kTraceSites && threadIdx.x == 0 &&
+           blockIdx.x == 0 && blockIdx.y == 0;
+}
+__device__ __forceinline__ void trace_word(const DevParams& p, int tslot, int k, int v) {
+    const_cast<int*>(p.o2_base)[p.J * p.L + tslot * kTraceW + k] = v;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1047,11 +1058,10 @@ __device__ __forceinline__ void family_cols_modlp(float2* U, int nb, int bs, int
                                                   float scale, float* S, float* outd) {
     constexpr int NN = FAM << K;
     if constexpr (FAM > 0 && NN <= HI && NN <= wstfft::kMaxFamilyN) {
-        if constexpr (NN >= 2) {
+        // RS > 0 belongs to the fused 48-point rows only: no other size is compiled for it
+        if constexpr (NN >= 2 && (RS == 0 || fused_row_n2(NN) == RS)) {
             if (rows == NN) {
-                // RS belongs to the fused 48-point rows only (the other sizes never meet it)
-                constexpr int RSN = fused_row_n2(NN) == RS ? RS : 0;
-                cols_modlp<NN, RSN>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
+                cols_modlp<NN, RS>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
                 return;
             }
         }
@@ -1736,8 +1746,10 @@ __device__ __forceinline__ void prep_body(unsigned char* smem, const DevParams& 
     const long long img = img0 + local;
     const int inM = p.pre_pad ? PM : p.M, inN = p.pre_pad ? PN : p.N;
     const float* x = in + local * inM * inN;
-    trace_word(p, lay.tslot, 0, tr_kernel(kTkPrep, FM, FN, 0, 0, 0));
-    trace_word(p, lay.tslot, 1, tr_prep(PC, wide_lowpass(p) ? (mfma_rc_ok<PC>() ? kLpMfmaRc : kLpMfma) : kLpPlain));
+    if (tracing(p, lay.tslot)) {
+        trace_word(p, lay.tslot, 0, tr_kernel(kTkPrep, FM, FN, 0, 0, 0));
+        trace_word(p, lay.tslot, 1, tr_prep(PC, wide_lowpass(p) ? (mfma_rc_ok<PC>() ? kLpMfmaRc : kLpMfma) : kLpPlain));
+    }
     float part = 0.f;
     for (GridIter it(PN); it.u < PM; it.next()) {
         const int su = p.pre_pad ? it.u : reflect_index(it.u - p.padTop, p.M);
@@ -1848,7 +1860,7 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     // 0.78 -> 0.79, so the exported-spectrum kernels keep the separate fold)
     constexpr bool FUSE1 = SQ && N1C >= kFuse1Min && wstfft::LineFFT<(N1C > 0 ? N1C : 2), true>::N2 > 1;
     const bool fused1 = FUSE1 && j1 == 0;
-    {
+    if (tracing(p, lay.tslot)) {
         const int s1 = 1 << j1;
         const int f1 = fused1 ? 0 : s1 == 1 ? 1 : s1 == 2 ? 2 : use_box1 ? 3 : s1 == 4 ? 4 : 5;
         const int lp1 = SQ ? kLpTap : wide_lowpass(p) ? (mfma_rc_ok<N1C>() ? kLpMfmaRc : kLpMfma) : kLpPlain;
@@ -2062,26 +2074,6 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
     const long long img = img0 + local;
     const float2* Hg = hexp + item * hspec_stride(nM1, hld, lay.hext);
     const float2* H = HG ? Hg : reinterpret_cast<const float2*>(smem);
-    {
-        constexpr int spec = HG ? 0 : (N1C > 0 && wstfft::LineFFT<(N1C > 0 ? N1C : 2), false>::N2 > 1) ? 1 : 2;
-        int branch = 7;
-        if constexpr (N1C > 0) {
-            branch = 1;
-        } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {
-            constexpr int N2C = unique_level(FM, MAXN);
-            branch = (j2first == j1 + 1 && (PM >> j1) == N2C && PM == PN) ? 2 : (PM >> j2first) == N2C ? 3 : 4;
-        } else if constexpr (!SQ && HG == 1 && FM == FN && FM > 0) {
-            branch = 6;
-            if (PM == PN && j2first == j1 + 1)
-                wstfft::static_for<0, 8>([&](auto mc) {
-                    constexpr int N1X = FM << decltype(mc)::value;
-                    if constexpr (N1X <= MAXN && N1X > prev_cap(MAXN))
-                        if ((PM >> j1) == N1X) branch = 5;
-                });
-        }
-        trace_word(p, lay.tslot, 0, tr_kernel(kTkO2, FM, FN, MAXN, SQ, HG));
-        trace_word(p, lay.tslot, 1, tr_o2(OC, LC, N1C, spec, branch));
-    }
 
     if constexpr (!HG) {
         // 1. half spectrum rows -> LDS, then the column FFTs (rows digit-reversed -> natural)
@@ -2125,14 +2117,6 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
         const int ld2 = odd_ld(nN2);
         const int pslot = nM2 * ld2;
         const int s2 = 1 << (j2 - j1);
-        {
-            constexpr int fk = FUSE ? kFdFused : (N1F > 0 && SC == 2) ? kFdTileS2
-                             : (N1F > 0 && (SC == 4 || SC == 8)) ? kFdTileList : 0;
-            const int lpk = SQ ? kLpTap : wide_lowpass(p) ? (mfma_rc_ok<NC>() ? kLpMfmaRc : kLpMfma) : kLpPlain;
-            if (2 + (j2 - j1 - 1) < kTraceW)
-                trace_word(p, lay.tslot, 2 + (j2 - j1 - 1),
-                       tr_level(j2, PB, SC, NC, fk ? fk : (s2 == 2 ? kFdDenseS2 : kFdBox), lpk, s2));
-        }
         int pb = lay.bcap / pslot;                 // paths per batch (multiple of 2)
         pb = PB ? PB : max(2, min(pb & ~1, 2 * nq));
 #pragma unroll 1
@@ -2211,75 +2195,110 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             // that batch's transform barriers (emit above reads S alone)
         }
     };
-    if constexpr (N1C > 0) {
-        // compile-time level sizes N1C / 2^k (the paths of an SQ launch start at j2 = j1 + 1)
-        wstfft::static_for<1, 8>([&](auto kc) {
-            constexpr int k = decltype(kc)::value;
-            constexpr int NN2 = N1C >> k;
-            if constexpr ((NN2 << k) == N1C && NN2 >= 1)
-                if (j1 + k < J && j1 + k >= j2first)
-                    level(j1 + k, NN2, NN2,
-                          std::integral_constant<int, LC == 0 ? 0 : (k == 1 && MAXN > kWholeFirstCap) ? 2 : LC>{},
-                          std::integral_constant<int, (1 << k)>{}, std::integral_constant<int, NN2>{});
-        });
-    } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {
-        // after a big level the paths start at the first LDS-resident level, which is the
-        // family's single size of this class (> 136 / 2): compile-time sizes from there on
-        // (runtime sizes when a plan stages that level too and starts further down)
-        constexpr int N2C = unique_level(FM, MAXN);
-        if (j2first == j1 + 1 && (PM >> j1) == N2C && PM == PN) {
-            // exported spectrum of a resident level of the class's single size (k_o1 finished
-            // the column FFTs): compile-time path sizes N2C / 2^k and tile-mapped folds from HBM
+    // The order-2 levels of this launch and their compile-time shapes, in one place: `fn` is
+    // called once per level as fn(branch, j2, nM2, nN2, PB, SC, NC).  The trace pass (below) and
+    // the work run the same dispatch, so the trace records the path the work takes.
+    auto dispatch = [&](auto&& fn, int& br) __attribute__((always_inline)) {
+        br = 7;
+        if constexpr (N1C > 0) {
+            br = 1;
+            // compile-time level sizes N1C / 2^k (the paths of an SQ launch start at j2 = j1 + 1)
             wstfft::static_for<1, 8>([&](auto kc) {
                 constexpr int k = decltype(kc)::value;
-                constexpr int NN2 = N2C >> k;
-                if constexpr ((NN2 << k) == N2C && NN2 >= 1)
-                    if (j1 + k < J)
-                        level(j1 + k, NN2, NN2, std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
+                constexpr int NN2 = N1C >> k;
+                if constexpr ((NN2 << k) == N1C && NN2 >= 1)
+                    if (j1 + k < J && j1 + k >= j2first)
+                        fn(j1 + k, NN2, NN2,
+                              std::integral_constant<int, LC == 0 ? 0 : (k == 1 && MAXN > kWholeFirstCap) ? 2 : LC>{},
                               std::integral_constant<int, (1 << k)>{}, std::integral_constant<int, NN2>{});
             });
-        } else if ((PM >> j2first) == N2C) {
-            wstfft::static_for<0, 8>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                constexpr int NN2 = N2C >> k;
-                if constexpr ((NN2 << k) == N2C && NN2 >= 1)
-                    if (j2first + k < J) level(j2first + k, NN2, NN2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
-                  std::integral_constant<int, 0>{});
-            });
-        } else {
-            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
-                  std::integral_constant<int, 0>{});
-        }
-    } else if constexpr (!SQ && HG == 1 && FM == FN && FM > 0) {
-        // exported-spectrum k_o2 (f3 / c1): a square level of one of the family's sizes in this
-        // class runs with compile-time path sizes (and, with LC, compile-time batch shapes)
-        bool done = false;
-        if (PM == PN && j2first == j1 + 1) {
-            wstfft::static_for<0, 8>([&](auto mc) {
-                constexpr int N1X = FM << decltype(mc)::value;
-                if constexpr (N1X <= MAXN && N1X > prev_cap(MAXN)) {
-                    if (!done && (PM >> j1) == N1X) {
-                        done = true;
-                        wstfft::static_for<1, 8>([&](auto kc) {
-                            constexpr int k = decltype(kc)::value;
-                            constexpr int NN2 = N1X >> k;
-                            if constexpr ((NN2 << k) == N1X && NN2 >= 1)
-                                if (j1 + k < J)
-                                    level(j1 + k, NN2, NN2,
-                                          std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
-                                          std::integral_constant<int, 0>{}, std::integral_constant<int, NN2>{});
-                        });
+        } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {
+            // after a big level the paths start at the first LDS-resident level, which is the
+            // family's single size of this class (> 136 / 2): compile-time sizes from there on
+            // (runtime sizes when a plan stages that level too and starts further down)
+            constexpr int N2C = unique_level(FM, MAXN);
+            if (j2first == j1 + 1 && (PM >> j1) == N2C && PM == PN) {
+                br = 2;
+                // exported spectrum of a resident level of the class's single size (k_o1 finished
+                // the column FFTs): compile-time path sizes N2C / 2^k and tile-mapped folds from HBM
+                wstfft::static_for<1, 8>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    constexpr int NN2 = N2C >> k;
+                    if constexpr ((NN2 << k) == N2C && NN2 >= 1)
+                        if (j1 + k < J)
+                            fn(j1 + k, NN2, NN2, std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
+                                  std::integral_constant<int, (1 << k)>{}, std::integral_constant<int, NN2>{});
+                });
+            } else if ((PM >> j2first) == N2C) {
+                br = 3;
+                wstfft::static_for<0, 8>([&](auto kc) {
+                    constexpr int k = decltype(kc)::value;
+                    constexpr int NN2 = N2C >> k;
+                    if constexpr ((NN2 << k) == N2C && NN2 >= 1)
+                        if (j2first + k < J) fn(j2first + k, NN2, NN2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+                      std::integral_constant<int, 0>{});
+                });
+            } else {
+                br = 4;
+                for (int j2 = j2first; j2 < J; ++j2) fn(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+                      std::integral_constant<int, 0>{});
+            }
+        } else if constexpr (!SQ && HG == 1 && FM == FN && FM > 0) {
+            // exported-spectrum k_o2 (f3 / c1): a square level of one of the family's sizes in this
+            // class runs with compile-time path sizes (and, with LC, compile-time batch shapes)
+            bool done = false;
+            br = 6;
+            if (PM == PN && j2first == j1 + 1) {
+                wstfft::static_for<0, 8>([&](auto mc) {
+                    constexpr int N1X = FM << decltype(mc)::value;
+                    if constexpr (N1X <= MAXN && N1X > prev_cap(MAXN)) {
+                        if (!done && (PM >> j1) == N1X) {
+                            done = true;
+                            br = 5;
+                            wstfft::static_for<1, 8>([&](auto kc) {
+                                constexpr int k = decltype(kc)::value;
+                                constexpr int NN2 = N1X >> k;
+                                if constexpr ((NN2 << k) == N1X && NN2 >= 1)
+                                    if (j1 + k < J)
+                                        fn(j1 + k, NN2, NN2,
+                                              std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
+                                              std::integral_constant<int, 0>{}, std::integral_constant<int, NN2>{});
+                            });
+                        }
                     }
-                }
-            });
+                });
+            }
+            if (!done)
+                for (int j2 = j2first; j2 < J; ++j2) fn(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+                      std::integral_constant<int, 0>{});
+        } else {
+            for (int j2 = j2first; j2 < J; ++j2) fn(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
+                      std::integral_constant<int, 0>{});
         }
-        if (!done)
-            for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
-                  std::integral_constant<int, 0>{});
-    } else {
-        for (int j2 = j2first; j2 < J; ++j2) level(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
-                  std::integral_constant<int, 0>{});
+    };
+    if (tracing(p, lay.tslot)) {
+        // trace pass: the same dispatch with a functor that only records each level's path
+        constexpr int spec = HG ? 0 : (N1C > 0 && wstfft::LineFFT<(N1C > 0 ? N1C : 2), false>::N2 > 1) ? 1 : 2;
+        int br = 0;
+        const int lpw = wide_lowpass(p) ? 1 : 0;
+        dispatch([&](int j2, int, int, auto pbc, auto scc, auto ncc) __attribute__((always_inline)) {
+            constexpr int PB = decltype(pbc)::value, SC = decltype(scc)::value, NC = decltype(ncc)::value;
+            constexpr int N1F = (SQ && NC > 0 && SC > 0) ? NC * SC : 0;
+            constexpr bool FUSE = N1F > 0 && SC == 2 && N1F / 2 >= kFuseMin &&
+                                  wstfft::LineFFT<(N1F > 0 ? N1F / 2 : 2), true>::N2 > 1;
+            constexpr int fk = FUSE ? kFdFused : (N1F > 0 && SC == 2) ? kFdTileS2
+                             : (N1F > 0 && (SC == 4 || SC == 8)) ? kFdTileList : 0;
+            const int s2 = 1 << (j2 - j1);
+            const int lpk = SQ ? kLpTap : lpw ? (mfma_rc_ok<NC>() ? kLpMfmaRc : kLpMfma) : kLpPlain;
+            if (2 + (j2 - j1 - 1) < kTraceW)
+                trace_word(p, lay.tslot, 2 + (j2 - j1 - 1),
+                           tr_level(j2, PB, SC, NC, fk ? fk : (s2 == 2 ? kFdDenseS2 : kFdBox), lpk, s2));
+        }, br);
+        trace_word(p, lay.tslot, 0, tr_kernel(kTkO2, FM, FN, MAXN, SQ, HG));
+        trace_word(p, lay.tslot, 1, tr_o2(OC, LC, N1C, spec, br));
     }
+    int br_run = 0;
+    dispatch(level, br_run);
 }
 
 

@@ -140,7 +140,6 @@ struct wst_plan {
     wst::Geometry g;
     int device = 0;
     bool host_only = false;     // wst_describe_variants: structure only, no device allocations
-    int* d_trace = nullptr;     // variant trace buffer (wst_plan_trace)
     std::vector<int> box1_l0;   // per scale j: box1_off of (j, l = 0) (host mirror of k_o1)
     DevParams dp{};
     // device allocations
@@ -228,7 +227,6 @@ void free_plan(wst_plan* p) {
         delete p;
         return;
     }
-    (void)hipFree(p->d_trace);
     (void)hipFree(p->d_psi);
     (void)hipFree(p->d_psi_off);
     (void)hipFree(p->d_lp);
@@ -800,7 +798,8 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
             }
         }
     t.tw_off.back() = static_cast<int>(tw.size());
-    std::vector<int> o2(static_cast<size_t>(J) * L, 0);
+    // (the variant-trace words of wst_plan_trace live after the J L coefficient bases)
+    std::vector<int> o2(static_cast<size_t>(J) * L + static_cast<size_t>(wstdev::kTraceSites) * wstdev::kTraceW, 0);
     {
         int k = 1 + J * L;
         for (int j1 = 0; j1 < J; ++j1)
@@ -845,7 +844,7 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
     {
         // phase-skipping timing ablation: diagnostic builds only (the results are wrong by design)
         const char* dbg = diag_env("WST_DEBUG_SKIP");
-        dp.dbg_skip = dbg ? std::atoi(dbg) : 0;
+        dp.flags = dbg ? (std::atoi(dbg) & 0x3fffffff) : 0;
     }
     dp.psi = plan->d_psi; dp.psi_off = plan->d_psi_off;
     dp.lp = plan->d_lp; dp.lp_off = plan->d_lp_off;
@@ -1834,24 +1833,24 @@ int wst_plan_trace(wst_plan* plan, int enable) {
     if (!plan) return fail(WST_ERR_INVALID, "plan is NULL");
     if (plan->host_only) return fail(WST_ERR_INVALID, "host-only plan");
     if (!enable) {
-        plan->dp.vtrace = nullptr;
+        plan->dp.flags &= ~kFlagTrace;
         return WST_OK;
     }
     const size_t bytes = static_cast<size_t>(kTraceSites) * kTraceW * sizeof(int);
-    if (!plan->d_trace) WST_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&plan->d_trace), bytes));
-    WST_HIP_CHECK(hipMemset(plan->d_trace, 0, bytes));
-    plan->dp.vtrace = plan->d_trace;
+    WST_HIP_CHECK(hipMemset(plan->d_o2 + static_cast<size_t>(plan->g.J) * plan->g.L, 0, bytes));
+    plan->dp.flags |= kFlagTrace;
     return WST_OK;
 }
 
 int wst_plan_read_trace(const wst_plan* plan, int32_t* out, int64_t max_words, int64_t* nwords) {
     if (!plan || !out || !nwords) return fail(WST_ERR_INVALID, "plan/out/nwords is NULL");
-    if (!plan->d_trace) return fail(WST_ERR_INVALID, "tracing was never enabled (wst_plan_trace)");
+    if (!(plan->dp.flags & kFlagTrace)) return fail(WST_ERR_INVALID, "tracing is off (wst_plan_trace)");
     const int64_t n = std::min<int64_t>(static_cast<int64_t>(describe_chunk(plan).size()),
                                         static_cast<int64_t>(kTraceSites) * kTraceW);
     if (max_words < n) return fail(WST_ERR_INVALID, "output buffer too small");
     WST_HIP_CHECK(hipDeviceSynchronize());
-    WST_HIP_CHECK(hipMemcpy(out, plan->d_trace, static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToHost));
+    WST_HIP_CHECK(hipMemcpy(out, plan->d_o2 + static_cast<size_t>(plan->g.J) * plan->g.L,
+                            static_cast<size_t>(n) * sizeof(int), hipMemcpyDeviceToHost));
     *nwords = n;
     return WST_OK;
 }

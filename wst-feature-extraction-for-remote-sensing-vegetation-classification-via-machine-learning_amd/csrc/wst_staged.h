@@ -112,10 +112,13 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
     const float2* gtw = level_tw(p, a.lvl, 1);
     for (int i = threadIdx.x; i < n; i += T) tw[i] = gtw[i];
     int nlines = a.rows;
-    wstdev::trace_word(p, a.tslot, 0, wstdev::tr_kernel(wstdev::kTkBigRows, 0, 0, N, 0, INV ? 1 : 0));
-    wstdev::trace_word(p, a.tslot, 1,
-                       wstdev::tr_big(a.mode, a.fold_all, a.mode == kRowFold1 ? (a.j1 == 0 ? 1 : 2) : 0,
-                                      (a.mode == kRowFold2 && !a.fold_all && a.box && a.n1 / n >= 4) ? 1 : 0, 0, 0, 0));
+    if (wstdev::tracing(p, a.tslot)) {
+        wstdev::trace_word(p, a.tslot, 0, wstdev::tr_kernel(wstdev::kTkBigRows, 0, 0, N, 0, INV ? 1 : 0));
+        wstdev::trace_word(p, a.tslot, 1,
+                           wstdev::tr_big(a.mode, a.fold_all, a.mode == kRowFold1 ? (a.j1 == 0 ? 1 : 2) : 0,
+                                          (a.mode == kRowFold2 && !a.fold_all && a.box && a.n1 / n >= 4) ? 1 : 0,
+                                          0, 0, 0));
+    }
 
     if (a.mode == kRowPad) {
         // arr = chunk-local plane; raw values first (S0 partials), then mean-centred
@@ -356,10 +359,12 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
     const int nc = min(C, a.ncols - c0);
     const float2* gtw = level_tw(p, a.lvl, 0);
     for (int i = threadIdx.x; i < n; i += T) tw[i] = gtw[i];
-    wstdev::trace_word(p, a.tslot, 0, wstdev::tr_kernel(wstdev::kTkBigCols, 0, 0, N, 0, INV ? 1 : 0));
-    wstdev::trace_word(p, a.tslot, 1,
-                       wstdev::tr_big(a.mode, 0, 0, 0, a.mode == kColModLp && p.oM > 8 ? 1 : 0,
-                                      a.mode == kColModLp ? a.g_lds : 0, a.uout ? 1 : 0));
+    if (wstdev::tracing(p, a.tslot)) {
+        wstdev::trace_word(p, a.tslot, 0, wstdev::tr_kernel(wstdev::kTkBigCols, 0, 0, N, 0, INV ? 1 : 0));
+        wstdev::trace_word(p, a.tslot, 1,
+                           wstdev::tr_big(a.mode, 0, 0, 0, a.mode == kColModLp && p.oM > 8 ? 1 : 0,
+                                          a.mode == kColModLp ? a.g_lds : 0, a.uout ? 1 : 0));
+    }
     float2* src = a.dst + static_cast<long long>(arr) * n * a.ncols;
     // kLoadBatch loads per thread in flight before their LDS stores (a load-store loop waits out
     // the HBM latency once per element: ~2.2 TB/s at c5)
