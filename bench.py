@@ -145,7 +145,7 @@ def rocprof_name(slot, PM, PN, J):
     if j1 < rb:
         n = PM >> j1
         if kind == "k_o1":
-            return f"k_big_rows<{n}, 1> + k_big_cols<{n}, 1> + k_big_final + U1hat k_big_rows/cols<{n}, 0>"
+            return f"k_big_rows<{n}, 1> + k_big_cols<{n}, 1> + k_big_final + U1hat k_big_rows<{n}, 0>"
         return f"staged order-2 k_big_rows/cols + k_big_final + k_o2<{fm}, {fn}, 136, 1, 1"
     n = max(PM, PN) >> j1
     cap = 12 if n <= 12 else 24 if n <= 24 else 48 if n <= 48 else 136
@@ -248,7 +248,7 @@ def staged_sequence(PM, PN, J, L, nst, max_order=2):
         seq += [(o1, big("rows", n1, True)), (o1, big("cols", m1, True)), (o1, "k_big_final")]
         if not do2:
             continue
-        seq += [(o1, big("rows", n1, False)), (o1, big("cols", m1, False))]
+        seq += [(o1, big("rows", n1, False))]      # kRowHalf: U1hat from the column spectra
         for j2 in range(j1 + 1, nst):
             seq += [(o2, big("rows", PN >> j2, True)), (o2, big("cols", PM >> j2, True))] * L
             seq.append((o2, "k_big_final"))

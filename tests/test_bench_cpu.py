@@ -45,9 +45,11 @@ def test_rocprof_names():
 
 
 def test_staged_slot_traffic_from_dispatch_sequence():
-    # c5 (384^2, J=6, L=12, square family 3: rb = nst = 2): one chunk = 41 staged launches
+    # c5 (384^2, J=6, L=12, square family 3: rb = nst = 2): one chunk = 39 staged launches
+    # (S0 + Xhat 4; per staged j1: order 1 3 + U1hat half rows 1; j1 = 0's 192^2 order 2 24 + final
+    # + HG k_o2; j1 = 1's HG k_o2)
     seq = bench.staged_sequence(384, 384, 6, 12, 2)
-    assert len(seq) == 4 + 5 + (2 * 12 + 1 + 1) + 5 + 1
+    assert len(seq) == 4 + 4 + (2 * 12 + 1 + 1) + 4 + 1
     assert seq[-1] == ("k_o2_j1=1", "k_o2<3, 3, 136, 1, 1>")
     # a recorded run: two chunks, each followed by resident kernels, one byte count per launch
     disp = []

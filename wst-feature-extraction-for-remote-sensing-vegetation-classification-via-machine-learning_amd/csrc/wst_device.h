@@ -177,10 +177,10 @@ constexpr int tr_level(int j2, int pb, int sc, int nc, int fold, int lp, int s2)
     return 1 | (tr_log2(s2) << 1) | (lp << 5) | (fold << 7) | (nc << 10) | ((sc ? tr_log2(sc) : 0) << 18) |
            (pb << 21) | (j2 << 26);
 }
-// staged passes: mode | fold_all | order-1 fold form (1 s = 1, 2 s > 1) | box fold | wide maps |
-// tap matrix in LDS | U stored
+// staged passes: mode (3 bits) | fold_all | order-1 fold form (1 s = 1, 2 s > 1) | box fold | wide
+// maps | tap matrix in LDS | U stored
 constexpr int tr_big(int mode, int fold_all, int fold1, int box, int wide, int glds, int ustore) {
-    return mode | (fold_all << 2) | (fold1 << 3) | (box << 5) | (wide << 6) | (glds << 7) | (ustore << 8);
+    return mode | (fold_all << 3) | (fold1 << 4) | (box << 6) | (wide << 7) | (glds << 8) | (ustore << 9);
 }
 // The writer of a site: lane 0 of workgroup 0, only while tracing.  Callers wrap the whole
 // word computation in `if (tracing(p, tslot))` so a production launch (kFlagTrace clear) skips

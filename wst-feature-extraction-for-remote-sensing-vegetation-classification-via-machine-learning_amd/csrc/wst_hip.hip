@@ -80,12 +80,11 @@ const FamilyOps* family_ops(int fm, int fn) {
 int cap_for(int n) { return n <= 12 ? 12 : n <= 24 ? 24 : n <= 48 ? 48 : 136; }
 constexpr int kBigRows = 8;   // rows per row-pass workgroup of the staged levels (kRowFold2: 2 paths)
 // Rows per row-pass workgroup by mode: the LDS holds 2 kBigRows lines, so the single-path modes
-// take 2 kBigRows rows and kRowReal2 (two rows per complex line) 4 kBigRows, when the row count
-// allows (at n = 384 the 8-line FFT stages left half the 256 threads idle, kRowReal2 three
-// quarters); otherwise the largest power of two dividing it (the grid has nrows / rows blocks;
-// order-2 levels have even row counts, so kRowReal2 keeps at least one row pair).
+// take 2 kBigRows rows when the row count allows (at n = 384 the 8-line FFT stages left half the
+// 256 threads idle); otherwise the largest power of two dividing it (the grid has nrows / rows
+// blocks).  kRowHalf sets its own (m/2 + 1 rows, ragged last block).
 int big_rows(int mode, int nrows) {
-    int r = mode == wstbig::kRowFold2 ? kBigRows : mode == wstbig::kRowReal2 ? 4 * kBigRows : 2 * kBigRows;
+    int r = mode == wstbig::kRowFold2 ? kBigRows : 2 * kBigRows;
     while (r > 1 && nrows % r != 0) r /= 2;
     return r;
 }
@@ -198,7 +197,7 @@ struct wst_plan {
     std::vector<int> fold_all_rows;               // per staged level: rows of the all-paths s = 2
     std::vector<size_t> fold_all_lds;             //   order-2 row pass (0: per-pair passes)
     std::vector<size_t> ws_hbig;                  // U1hat half spectra of staged j1 (per plane)
-    size_t ws_tmp = 0, ws_ureal = 0, ws_part = 0, ws_csum = 0, ws_mean = 0;
+    size_t ws_tmp = 0, ws_colt = 0, ws_part = 0, ws_csum = 0, ws_mean = 0;
     int64_t max_chunk = 2048;                     // planes per workspace chunk
     // workspace per plane: Xhat, then the half spectra of every j1 < J-1
     size_t ws_xhat = 0;
@@ -950,7 +949,8 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
         if (!do2) continue;
         plan->ws_hbig[j1] = wsp;
         wsp += align16(static_cast<size_t>(L) * m1 * (n1 / 2 + 1) * sizeof(float2));
-        plan->ws_ureal = std::max(plan->ws_ureal, static_cast<size_t>(L) * m1 * n1 * sizeof(float));
+        // column spectra of U1, rows 0..m1/2 (kColModLpFwd -> kRowHalf)
+        plan->ws_colt = std::max(plan->ws_colt, static_cast<size_t>(L) * (m1 / 2 + 1) * n1 * sizeof(float2));
         for (int j2 = j1 + 1; j2 < plan->nst; ++j2) {
             const size_t m2 = static_cast<size_t>(g.PM >> j2), n2 = static_cast<size_t>(g.PN >> j2);
             tmp_c = std::max(tmp_c, static_cast<size_t>(L) * m2 * n2);
@@ -994,9 +994,9 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
     if (plan->rb > 0) {
         plan->ws_tmp = wsp;
         wsp += align16(tmp_c * sizeof(float2));
-        const size_t ureal_bytes = plan->ws_ureal;
-        plan->ws_ureal = wsp;
-        wsp += align16(ureal_bytes);
+        const size_t colt_bytes = plan->ws_colt;
+        plan->ws_colt = wsp;
+        wsp += align16(colt_bytes);
         plan->ws_part = wsp;
         wsp += align16(part_n * noms * sizeof(float));
         plan->ws_csum = wsp;
@@ -1346,7 +1346,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
     const auto& cm = wstlaunch::wst_big_common_ops();
     float2* xhat = reinterpret_cast<float2*>(base);
     float2* tmp = reinterpret_cast<float2*>(base + plan->ws_tmp * chunk);
-    float* ureal = reinterpret_cast<float*>(base + plan->ws_ureal * chunk);
+    float2* colt = reinterpret_cast<float2*>(base + plan->ws_colt * chunk);
     float* part = reinterpret_cast<float*>(base + plan->ws_part * chunk);
     float* csum = reinterpret_cast<float*>(base + plan->ws_csum * chunk);
     // [plane][kMeanParts] partial sums, then [plane * L + l1] U1 means
@@ -1416,9 +1416,10 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         a.j1 = j1;
         a.dst = tmp;
         plan->big_r[j1]->rows(true, Launch{dim3(m1 / a.rows, nimg * L), tb, plan->big_rows_lds[j1], stream}, dp, a);
-        BigArgs c = cargs(kColModLp, j1, n1);
+        // (order 2 follows: the column pass also forms the column spectra of U1, kColModLpFwd)
+        BigArgs c = cargs(do2 ? kColModLpFwd : kColModLp, j1, n1);
         c.dst = tmp;
-        c.uout = do2 ? ureal : nullptr;
+        c.colt = do2 ? colt : nullptr;
         c.vpart = part;
         c.csum = csum;
         c.scale = 1.f / (static_cast<float>(g.PM) * static_cast<float>(g.PN));
@@ -1427,16 +1428,17 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         cm.final_(Launch{dim3(nimg * L), dim3(64), sbytes, stream}, dp, kFinalCols, 1, n1, m1, noms, part,
                   gnat(j1, 1), csum, do2 ? umean : nullptr, L, j1, 0, 0, 1, img0, d_out, pooled);
         if (do2) {
-            // U1hat = fft2(U1 - mean) as half spectra (natural order) for the order-2 folds
-            BigArgs r2 = rargs(kRowReal2, j1);
-            r2.ureal = ureal;
+            // U1hat = fft2(U1 - mean) as half spectra (natural order) for the order-2 folds: the
+            // row transforms of the column spectra's rows 0..m1/2, written with their mirrors
+            BigArgs r2 = rargs(kRowHalf, j1);
+            r2.nrows = m1 / 2 + 1;
+            r2.rows = 2 * kBigRows;
+            r2.colt = colt;
+            r2.csum = csum;
             r2.mean = umean;
             r2.dst = hbig;
-            plan->big_r[j1]->rows(false, Launch{dim3(m1 / r2.rows, nimg * L), tb, plan->big_rows_lds[j1], stream},
-                                  dp, r2);
-            BigArgs c2 = cargs(kColStore, j1, hld);
-            c2.dst = hbig;
-            plan->big_c[j1]->cols(false, Launch{col_grid(hld, nimg * L), tb, plan->big_cols_lds[j1], stream}, dp, c2);
+            plan->big_r[j1]->rows(false, Launch{dim3((r2.nrows + r2.rows - 1) / r2.rows, nimg * L), tb,
+                                                plan->big_rows_lds[j1], stream}, dp, r2);
         }
         WST_HIP_CHECK(hipGetLastError());
         if ((rc = timer.end(stream, 1 + j1)) != WST_OK) return rc;
@@ -1775,10 +1777,9 @@ std::vector<int> describe_chunk(const wst_plan* pl) {
             const bool do2 = g.max_order >= 2 && j1 < J - 1;
             describe_big(d, true, pl->big_r[j1]->n, true, tr_big(kRowFold1, 0, j1 == 0 ? 1 : 2, 0, 0, 0, 0));
             describe_big(d, false, pl->big_c[j1]->n, true,
-                         tr_big(kColModLp, 0, 0, 0, wide_maps, pl->big_g_lds[j1], do2 ? 1 : 0));
+                         tr_big(do2 ? kColModLpFwd : kColModLp, 0, 0, 0, wide_maps, pl->big_g_lds[j1], 0));
             if (!do2) continue;
-            describe_big(d, true, pl->big_r[j1]->n, false, tr_big(kRowReal2, 0, 0, 0, 0, 0, 0));
-            describe_big(d, false, pl->big_c[j1]->n, false, tr_big(kColStore, 0, 0, 0, 0, 0, 0));
+            describe_big(d, true, pl->big_r[j1]->n, false, tr_big(kRowHalf, 0, 0, 0, 0, 0, 0));
             for (int j2 = j1 + 1; j2 < pl->nst; ++j2) {
                 const int m1 = g.PM >> j1, m2 = g.PM >> j2;
                 const bool fold_all = m1 == 2 * m2 && pl->fold_all_rows[j2] > 0;

@@ -6,13 +6,19 @@
 // kymatio steps around each transform are fused into the passes:
 //   k_big_rows (forward):  kRowPad   reflect-pad gather of the input plane, S0 row partials,
 //                                    mean removal (conditioning only, as k_prep)
-//                          kRowReal2 U1 - mean, two real rows packed per complex line, split into
-//                                    the two rows' Hermitian half spectra (as k_o1 step 4-5)
+//                          kRowHalf  rows 0..m/2 of the column-transformed U1 (kColModLpFwd), the
+//                                    global mean removed at row 0, forward row FFT, written with
+//                                    their Hermitian mirrors as the natural-order half spectra
 //   k_big_rows (inverse):  kRowFold1 fold_{2^j1}(Xhat * psi0) (order-1 subsample_fourier)
 //                          kRowFold2 Hermitian fold_{2^(j2-j1)}(U1hat * psi2 pair), 2 paths
 //   k_big_cols:            kColStore plain column transform
 //                          kColModLp |.| * scale, optional U store, phi low-pass column partials
 //                                    V[q][a] = sum_p GMnat[p][a] |z[p][q]| and column sums
+//                          kColModLpFwd  kColModLp, then the forward column FFT of U (two columns
+//                                    minus their own means per complex line) and its Hermitian
+//                                    split: rows 0..m/2 of each column's spectrum (order 2 follows;
+//                                    round 5: replaces a U store, a packed real-row pass and a
+//                                    column pass per staged j1)
 //   k_big_final:           S[a][c] from the partials (+ U1 mean), emitted like the LDS kernels
 // SURVEY.md Appendix A.4; reference call sites train_and_save_model.py:359-376.
 #pragma once
@@ -30,8 +36,8 @@ constexpr int kMeanParts = 16;                  // k_big_mean partial sums per p
 constexpr int kLoadBatch = 8;                   // global loads per thread in flight (tile loads)
 constexpr int kBigOGroup = 16;                  // outputs per accumulation round of wide low-passes
 
-enum RowMode { kRowPad = 0, kRowReal2 = 1, kRowFold1 = 2, kRowFold2 = 3 };
-enum ColMode { kColStore = 0, kColModLp = 1 };
+enum RowMode { kRowPad = 0, kRowFold1 = 2, kRowFold2 = 3, kRowHalf = 4 };   // (1: retired)
+enum ColMode { kColStore = 0, kColModLp = 1, kColModLpFwd = 2 };
 enum FinalMode { kFinalRows = 0, kFinalCols = 1 };
 
 // Arguments of one staged launch (POD, by value).  A level's arrays are nrows x ncols (PM >> r by
@@ -50,13 +56,11 @@ struct BigArgs {
     // kRowPad
     const float* in;
     const float* mean;           // kRowPad: plane sum partials (kMeanParts per plane);
-                                 // kRowReal2: (plane, l1) U1 means
+                                 // kRowHalf: (plane, l1) U1 means
     float* tpart;                // kRowPad: S0 row partials (nrows x oms per plane)
     // kRowFold1
     const float2* xhat;
     int j1;                      // kRowFold1: psi level-0 filters of scale j1; s = 2^j1
-    // kRowReal2
-    const float* ureal;          // U1 (nrows x n per array)
     // kRowFold2
     const float2* hsrc;          // half spectra at level j1 ((nrows s) x (n1/2+1) per (plane, l1))
     int n1, l1, j2;              // n1: row length at level j1 (= n s)
@@ -69,7 +73,8 @@ struct BigArgs {
                                  // read of the spectrum taps, one FFT pass over npath * rows lines
     // outputs
     float2* dst;
-    float* uout;                 // kColModLp: U real (optional)
+    float2* colt;                // kColModLpFwd: column spectra rows 0..m/2 ((m/2+1) x ncols per
+                                 // array); kRowHalf: their source (nrows = m/2 + 1 valid rows)
     float* vpart;                // kColModLp: V[q][a] (ncols x oms per array)
     float* csum;                 // kColModLp: column sums (ncols per array)
     float scale;                 // kColModLp
@@ -150,26 +155,19 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
             const int rr = i / n, q = i - (i / n) * n;
             A[rr * ld + q].x -= mu;
         }
-    } else if (a.mode == kRowReal2) {
-        // arr = (plane, l1); rows r0 .. r0 + rows - 1 packed in pairs
-        nlines = a.rows / 2;
-        const float* U = a.ureal + static_cast<long long>(arr) * m * n;
+    } else if (a.mode == kRowHalf) {
+        // arr = plane * L + l1; rows r0.. of the m/2 + 1 column-spectrum rows (a.nrows of them).
+        // Row 0 holds sum_p (U[p][q] - mu_q) (each column minus its own mean, kColModLpFwd); the
+        // global-mean-removed row is that + m (mu_q - mu) = + csum[q] - m mu.
+        nlines = min(a.rows, a.nrows - r0);
+        const float2* Cs = a.colt + static_cast<long long>(arr) * a.nrows * n;
+        const int mm = 2 * (a.nrows - 1);
         const float mu = a.mean[arr];
-        for (int i0 = threadIdx.x; i0 < nlines * n; i0 += kLoadBatch * T) {
-            float2 t2[kLoadBatch];
-#pragma unroll
-            for (int k = 0; k < kLoadBatch; ++k) {
-                const int i = min(i0 + k * T, nlines * n - 1);
-                const int t = i / n, q = i - (i / n) * n;
-                const int u = r0 + 2 * t;
-                t2[k] = make_float2(U[u * n + q], U[(u + 1) * n + q]);
-            }
-#pragma unroll
-            for (int k = 0; k < kLoadBatch; ++k) {
-                const int i = i0 + k * T;
-                const int t = i / n, q = i - (i / n) * n;
-                if (i < nlines * n) A[t * ld + q] = make_float2(t2[k].x - mu, t2[k].y - mu);
-            }
+        for (int i = threadIdx.x; i < nlines * n; i += T) {
+            const int t = i / n, q = i - (i / n) * n;
+            float2 v = wstdev::ldnt(Cs + static_cast<long long>(r0 + t) * n + q);
+            if (r0 + t == 0) v.x += a.csum[static_cast<long long>(arr) * n + q] - static_cast<float>(mm) * mu;
+            A[t * ld + q] = v;
         }
     } else if (a.mode == kRowFold1) {
         // arr = plane * L + l1: rows of fold_s(Xhat * psi0_{j1, l1}), Xhat is (m s) x (n s)
@@ -322,23 +320,63 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
     wstfft::EpiIdentity id;
     big_fft<N, INV>(A, wstfft::Lines(1, 0, nlines, ld, 1), n, tw, id);
 
+    if (a.mode == kRowHalf) {
+        // U1hat rows k1 = r0 + t (0 <= k1 <= m/2) as the natural-order half spectra (hld = n/2 + 1
+        // columns, m rows): row k1 directly, row m - k1 (0 < k1 < m/2) from the conjugate mirror
+        const int hld = n / 2 + 1, mm = 2 * (a.nrows - 1);
+        float2* D = a.dst + static_cast<long long>(arr) * mm * hld;
+        for (int i = threadIdx.x; i < nlines * hld; i += T) {
+            const int t = i / hld, c = i - (i / hld) * hld;
+            const int k1 = r0 + t;
+            wstdev::stnt(D + static_cast<long long>(k1) * hld + c, A[t * ld + c]);
+            if (k1 > 0 && 2 * k1 < mm) {
+                const float2 z = A[t * ld + (c == 0 ? 0 : n - c)];
+                wstdev::stnt(D + static_cast<long long>(mm - k1) * hld + c, make_float2(z.x, -z.y));
+            }
+        }
+        return;
+    }
     if (a.mode == kRowPad || a.mode == kRowFold1) {
         float2* D = a.dst + static_cast<long long>(arr) * m * n;
         for (int i = threadIdx.x; i < a.rows * n; i += T) {
             const int rr = i / n, q = i - (i / n) * n;
             wstdev::stnt(D + (r0 + rr) * n + q, A[rr * ld + q]);
         }
-    } else if (a.mode == kRowReal2) {
-        const int hld = n / 2 + 1;
-        float2* D = a.dst + static_cast<long long>(arr) * m * hld;
-        for (int i = threadIdx.x; i < nlines * hld; i += T) {
-            const int t = i / hld, q = i - (i / hld) * hld;
-            const float2 z = A[t * ld + q];
-            const float2 zm = A[t * ld + (q == 0 ? 0 : n - q)];
-            const int u = r0 + 2 * t;
-            wstdev::stnt(D + u * hld + q, make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y)));
-            wstdev::stnt(D + (u + 1) * hld + q, make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x)));
-        }
+    }
+}
+
+// kColModLpFwd tail: the tile's U columns (.x, |.| * scale) minus their own means, two per complex
+// line (column 2c' real, 2c' + 1 imaginary, in column 2c''s slots), forward n-point FFT, Hermitian
+// split into the two columns' spectra, rows 0..n/2 stored to colt ((n/2 + 1) x ncols per array).
+// Subtracting each column's own mean leaves row 0 ~ 0; kRowHalf restores the global-mean-removed
+// row 0 from the column sums (the conditioning of U - mu, which the packed real-row pass applied).
+template <int N>
+__device__ __forceinline__ void col_spectra(float2* A, const float2* tw, const BigArgs& a, int arr, int c0,
+                                            int nc, int n, const float* csum_t) {
+    const int ld = n | 1, T = blockDim.x, npair = (nc + 1) / 2;
+    const float inv_n = 1.f / static_cast<float>(n);
+    __syncthreads();   // column sums in csum_t; every lane done reading .x of the tile
+    for (int i = threadIdx.x; i < npair * n; i += T) {
+        const int cp = i / n, u = i - (i / n) * n;
+        const int ca = 2 * cp, cb = 2 * cp + 1;
+        const float re = A[ca * ld + u].x - csum_t[ca] * inv_n;
+        const float im = cb < nc ? A[cb * ld + u].x - csum_t[cb] * inv_n : 0.f;
+        A[ca * ld + u] = make_float2(re, im);
+    }
+    __syncthreads();
+    wstfft::EpiIdentity id;
+    big_fft<N, false>(A, wstfft::Lines(1, 0, npair, 2 * ld, 1), n, tw, id);
+    const int hrows = n / 2 + 1;
+    float2* D = a.colt + static_cast<long long>(arr) * hrows * a.ncols;
+    for (int i = threadIdx.x; i < hrows * kColTile; i += T) {
+        const int k1 = i / kColTile, c = i - (i / kColTile) * kColTile;
+        if (c >= nc) continue;
+        const int cp = c >> 1;
+        const float2 z = A[2 * cp * ld + k1];
+        const float2 zm = A[2 * cp * ld + (k1 == 0 ? 0 : n - k1)];
+        const float2 h = (c & 1) ? make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x))
+                                 : make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
+        wstdev::stnt(D + static_cast<long long>(k1) * a.ncols + c0 + c, h);
     }
 }
 
@@ -362,8 +400,8 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
     if (wstdev::tracing(p, a.tslot)) {
         wstdev::trace_word(p, a.tslot, 0, wstdev::tr_kernel(wstdev::kTkBigCols, 0, 0, N, 0, INV ? 1 : 0));
         wstdev::trace_word(p, a.tslot, 1,
-                           wstdev::tr_big(a.mode, 0, 0, 0, a.mode == kColModLp && p.oM > 8 ? 1 : 0,
-                                          a.mode == kColModLp ? a.g_lds : 0, a.uout ? 1 : 0));
+                           wstdev::tr_big(a.mode, 0, 0, 0, a.mode != kColStore && p.oM > 8 ? 1 : 0,
+                                          a.mode != kColStore ? a.g_lds : 0, 0));
     }
     float2* src = a.dst + static_cast<long long>(arr) * n * a.ncols;
     // kLoadBatch loads per thread in flight before their LDS stores (a load-store loop waits out
@@ -393,16 +431,11 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
         }
         return;
     }
-    // kColModLp: |.| * scale in place (.x), then partials over the rows of each column
+    // kColModLp / kColModLpFwd: |.| * scale in place (.x), then partials over the rows of each
+    // column (and, Fwd, the column spectra of U)
+    __shared__ float csum_t[C];   // kColModLpFwd: this tile's column sums
     wstdev::EpiModulus mod{a.scale, 0.f};
     big_fft<N, INV>(A, wstfft::Lines(1, 0, nc, ld, 1), n, tw, mod);
-    if (a.uout) {
-        float* U = a.uout + static_cast<long long>(arr) * n * a.ncols;
-        for (int i = threadIdx.x; i < n * C; i += T) {
-            const int u = i / C, c = i - (i / C) * C;
-            if (c < nc) U[static_cast<long long>(u) * a.ncols + c0 + c] = A[c * ld + u].x;
-        }
-    }
     // V[q][a] = sum_p GMnat[p][a] m[p][q] (a < oM) and the column sum: the taps are staged in LDS
     // after the column tile (when they fit), one thread per (column, 16-row chunk) accumulates
     // every output of its rows, then the 16 chunks of a column are shuffle-reduced
@@ -436,8 +469,10 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
             if (pc == 0) {
                 for (int k = 0; k < p.oM; ++k) a.vpart[(static_cast<long long>(arr) * a.ncols + c0 + c) * oms + k] = acc[k];
                 a.csum[static_cast<long long>(arr) * a.ncols + c0 + c] = acc[8];
+                csum_t[c] = acc[8];
             }
         }
+        if (a.mode == kColModLpFwd) col_spectra<N>(A, tw, a, arr, c0, nc, n, csum_t);
         return;
     }
     // wide output maps: kBigOGroup outputs per round over the column tile held in LDS
@@ -462,10 +497,14 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
             if (pc == 0) {
                 for (int k = 0; k < kBigOGroup && a0 + k < p.oM; ++k)
                     a.vpart[(static_cast<long long>(arr) * a.ncols + c0 + c) * oms + a0 + k] = acc[k];
-                if (a0 == 0) a.csum[static_cast<long long>(arr) * a.ncols + c0 + c] = acc[kBigOGroup];
+                if (a0 == 0) {
+                    a.csum[static_cast<long long>(arr) * a.ncols + c0 + c] = acc[kBigOGroup];
+                    csum_t[c] = acc[kBigOGroup];
+                }
             }
         }
     }
+    if (a.mode == kColModLpFwd) col_spectra<N>(A, tw, a, arr, c0, nc, n, csum_t);
 }
 
 // Size-independent kernels: defined in one object only (wst_staged.hip with WST_BIG_N = 0).

@@ -19,8 +19,8 @@ FOLD1 = {0: "fused_rowA", 1: "s1", 2: "s2", 3: "box", 4: "s4", 5: "runtime_s"}
 SPEC = {0: "hbm", 1: "rd_from", 2: "copy"}
 BRANCH = {1: "N1C", 2: "hg_ct_export", 3: "hg_ct_first", 4: "hg_runtime", 5: "exp_ct", 6: "exp_runtime",
           7: "runtime"}
-ROWMODE = {0: "pad", 1: "real2", 2: "fold1", 3: "fold2"}
-COLMODE = {0: "store", 1: "modlp"}
+ROWMODE = {0: "pad", 1: "real2", 2: "fold1", 3: "fold2", 4: "half"}
+COLMODE = {0: "store", 1: "modlp", 2: "modlp_fwd"}
 
 
 def _bits(v, lo, n):
@@ -51,11 +51,11 @@ def body_name(w0, w1):
     if kind == 3:
         return (f"OC={_bits(w1, 0, 4)} LC={_bits(w1, 4, 5)} N1C={_bits(w1, 9, 8)} "
                 f"spec={SPEC.get(_bits(w1, 17, 2), '?')} branch={BRANCH.get(_bits(w1, 19, 3), '?')}")
-    mode = _bits(w1, 0, 2)
+    mode = _bits(w1, 0, 3)
     if kind == 4:
-        return (f"mode={ROWMODE[mode]} fold_all={_bits(w1, 2, 1)} fold1={_bits(w1, 3, 2)} "
-                f"box={_bits(w1, 5, 1)}")
-    return f"mode={COLMODE.get(mode, mode)} wide={_bits(w1, 6, 1)} g_lds={_bits(w1, 7, 1)} u={_bits(w1, 8, 1)}"
+        return (f"mode={ROWMODE.get(mode, mode)} fold_all={_bits(w1, 3, 1)} fold1={_bits(w1, 4, 2)} "
+                f"box={_bits(w1, 6, 1)}")
+    return f"mode={COLMODE.get(mode, mode)} wide={_bits(w1, 7, 1)} g_lds={_bits(w1, 8, 1)} u={_bits(w1, 9, 1)}"
 
 
 def level_name(wl):
