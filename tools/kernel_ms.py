@@ -6,10 +6,12 @@ import numpy as np, torch, wst_amd  # noqa: F401
 from wst_amd import _lib
 if os.environ.get("AB_LIB"):          # A/B variant build in the package dir (tools/variant.sh)
     _lib.use_library(os.environ["AB_LIB"])
-# geometry: env WST_KM_GEOM="planes,M,J" (default the c2 step: 3072 planes of 64^2, J=4)
-B, M, J = (int(v) for v in os.environ.get("WST_KM_GEOM", "3072,64,4").split(","))
+# geometry: env WST_KM_GEOM="planes,M,J[,L]" (default the c2 step: 3072 planes of 64^2, J=4, L=8)
+_g = [int(v) for v in os.environ.get("WST_KM_GEOM", "3072,64,4").split(",")]
+B, M, J = _g[:3]
+LL = _g[3] if len(_g) > 3 else 8
 x = torch.from_numpy(np.random.default_rng(1).integers(0, 256, (B, M, M), dtype=np.uint8).astype(np.float32) / 255).cuda()
-plan = _lib.Plan(M, M, J, 8)
+plan = _lib.Plan(M, M, J, LL)
 out = torch.empty((B, plan.K, plan.Mo, plan.No), device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 nslot = 1 + 2 * J

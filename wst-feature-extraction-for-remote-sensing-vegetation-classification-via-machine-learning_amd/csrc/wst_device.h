@@ -126,8 +126,26 @@ struct LdsLayout {
     int hext;               // resident levels: an item's half spectrum in the workspace holds
                             // nM1 + 1 rows (row nM1 = row 0 for the tile folds' mirrored taps;
                             // written by an exporting k_o1, formed in LDS by k_o2 otherwise)
+#ifndef WST_NO_TSLOT       // (A/B builds: the layout without the field)
     int tslot;              // variant-trace site of this launch (kFlagTrace)
+#endif
 };
+__host__ __device__ inline void set_tslot(LdsLayout& l, int s) {
+#ifndef WST_NO_TSLOT
+    l.tslot = s;
+#else
+    (void)l;
+    (void)s;
+#endif
+}
+__host__ __device__ inline int get_tslot(const LdsLayout& l) {
+#ifndef WST_NO_TSLOT
+    return l.tslot;
+#else
+    (void)l;
+    return 0;
+#endif
+}
 
 // ------------------------------------------------------------------------------------------
 // Variant trace (tests: wst_plan_trace / wst_describe_variants, include/wst_hip.h).  With
@@ -1746,9 +1764,9 @@ __device__ __forceinline__ void prep_body(unsigned char* smem, const DevParams& 
     const long long img = img0 + local;
     const int inM = p.pre_pad ? PM : p.M, inN = p.pre_pad ? PN : p.N;
     const float* x = in + local * inM * inN;
-    if (tracing(p, lay.tslot)) {
-        trace_word(p, lay.tslot, 0, tr_kernel(kTkPrep, FM, FN, 0, 0, 0));
-        trace_word(p, lay.tslot, 1, tr_prep(PC, wide_lowpass(p) ? (mfma_rc_ok<PC>() ? kLpMfmaRc : kLpMfma) : kLpPlain));
+    if (tracing(p, get_tslot(lay))) {
+        trace_word(p, get_tslot(lay), 0, tr_kernel(kTkPrep, FM, FN, 0, 0, 0));
+        trace_word(p, get_tslot(lay), 1, tr_prep(PC, wide_lowpass(p) ? (mfma_rc_ok<PC>() ? kLpMfmaRc : kLpMfma) : kLpPlain));
     }
     float part = 0.f;
     for (GridIter it(PN); it.u < PM; it.next()) {
@@ -1860,12 +1878,12 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     // 0.78 -> 0.79, so the exported-spectrum kernels keep the separate fold)
     constexpr bool FUSE1 = SQ && N1C >= kFuse1Min && wstfft::LineFFT<(N1C > 0 ? N1C : 2), true>::N2 > 1;
     const bool fused1 = FUSE1 && j1 == 0;
-    if (tracing(p, lay.tslot)) {
+    if (tracing(p, get_tslot(lay))) {
         const int s1 = 1 << j1;
         const int f1 = fused1 ? 0 : s1 == 1 ? 1 : s1 == 2 ? 2 : use_box1 ? 3 : s1 == 4 ? 4 : 5;
         const int lp1 = SQ ? kLpTap : wide_lowpass(p) ? (mfma_rc_ok<N1C>() ? kLpMfmaRc : kLpMfma) : kLpPlain;
-        trace_word(p, lay.tslot, 0, tr_kernel(kTkO1, FM, FN, MAXN, SQ, 0));
-        trace_word(p, lay.tslot, 1, tr_o1(OC, N1C, fused1 ? 1 : 0, lp1, do2 ? 1 : 0, lay.export_full, f1));
+        trace_word(p, get_tslot(lay), 0, tr_kernel(kTkO1, FM, FN, MAXN, SQ, 0));
+        trace_word(p, get_tslot(lay), 1, tr_o1(OC, N1C, fused1 ? 1 : 0, lp1, do2 ? 1 : 0, lay.export_full, f1));
     }
     EpiModulus mod1{1.f / (static_cast<float>(PM) * static_cast<float>(PN)), 0.f};
     if (fused1) {
@@ -2276,7 +2294,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                       std::integral_constant<int, 0>{});
         }
     };
-    if (tracing(p, lay.tslot)) {
+    if (tracing(p, get_tslot(lay))) {
         // trace pass: the same dispatch with a functor that only records each level's path
         constexpr int spec = HG ? 0 : (N1C > 0 && wstfft::LineFFT<(N1C > 0 ? N1C : 2), false>::N2 > 1) ? 1 : 2;
         int br = 0;
@@ -2291,11 +2309,11 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             const int s2 = 1 << (j2 - j1);
             const int lpk = SQ ? kLpTap : lpw ? (mfma_rc_ok<NC>() ? kLpMfmaRc : kLpMfma) : kLpPlain;
             if (2 + (j2 - j1 - 1) < kTraceW)
-                trace_word(p, lay.tslot, 2 + (j2 - j1 - 1),
+                trace_word(p, get_tslot(lay), 2 + (j2 - j1 - 1),
                            tr_level(j2, PB, SC, NC, fk ? fk : (s2 == 2 ? kFdDenseS2 : kFdBox), lpk, s2));
         }, br);
-        trace_word(p, lay.tslot, 0, tr_kernel(kTkO2, FM, FN, MAXN, SQ, HG));
-        trace_word(p, lay.tslot, 1, tr_o2(OC, LC, N1C, spec, br));
+        trace_word(p, get_tslot(lay), 0, tr_kernel(kTkO2, FM, FN, MAXN, SQ, HG));
+        trace_word(p, get_tslot(lay), 1, tr_o2(OC, LC, N1C, spec, br));
     }
     int br_run = 0;
     dispatch(level, br_run);

@@ -445,8 +445,8 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
                                                   : 0;
         const auto fits = [&](size_t nl) {
             const size_t lines = std::max<size_t>(2 * kBigRows, wstbig::kColTile);
-            return (nl + lines * (nl | 1)) * sizeof(float2) + nl * tapw * sizeof(float) <=
-                   static_cast<size_t>(kMaxLds);
+            return (nl + lines * (nl | 1)) * sizeof(float2) + nl * tapw * sizeof(float) +
+                       wstbig::kColTile * sizeof(float) <= static_cast<size_t>(kMaxLds);
         };
         for (int r = 0; r < J && std::max(g.PM, g.PN) >> r > wstbig::kBigMinN; ++r) {
             const size_t nl = static_cast<size_t>(std::max(g.PM, g.PN) >> r);
@@ -888,12 +888,14 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
             plan->big_r[r] = big_ops(g.PN >> r);
             plan->big_c[r] = big_ops(g.PM >> r);
             plan->big_rows_lds[r] = (nn + 2 * kBigRows * (nn | 1)) * sizeof(float2);
+            // + tap matrix + the tile's column sums (kColModLpFwd)
             plan->big_cols_lds[r] = (nm + wstbig::kColTile * (nm | 1)) * sizeof(float2) +
-                                    nm * static_cast<size_t>(noms) * sizeof(float);   // + tap matrix
+                                    nm * static_cast<size_t>(noms) * sizeof(float) + wstbig::kColTile * sizeof(float);
             if (plan->big_cols_lds[r] > static_cast<size_t>(kMaxLds) && g.oM > 8) {
                 // wide output maps: the tap matrix stays in L2
                 plan->big_g_lds[r] = 0;
-                plan->big_cols_lds[r] = (nm + wstbig::kColTile * (nm | 1)) * sizeof(float2);
+                plan->big_cols_lds[r] = (nm + wstbig::kColTile * (nm | 1)) * sizeof(float2) +
+                                        wstbig::kColTile * sizeof(float);
             }
             if (std::max(plan->big_rows_lds[r], plan->big_cols_lds[r]) > static_cast<size_t>(kMaxLds))
                 return fail(WST_ERR_UNSUPPORTED, "level " + std::to_string(r) + " (" + std::to_string(nm) + "x" +
@@ -1301,7 +1303,7 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
     int rc;
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
     LdsLayout lay1 = plan->o1_lay[j1];
-    lay1.tslot = site++;
+    set_tslot(lay1, site++);
     if (!plan->ops->o1(plan->cap[j1], plan->sq,
                        Launch{dim3(nimg * g.L), dim3(plan->o1_threads[j1]), plan->o1_lds[j1], stream},
                        plan->dp, lay1, j1, nimg, img0, xhat, hexp, d_out, pooled))
@@ -1312,7 +1314,7 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
     if ((rc = timer.begin(stream)) != WST_OK) return rc;
     if (plan->o2_export[j1]) {   // spectrum exported fully transformed: fold from HBM
         LdsLayout lx = plan->o2x_lay[j1];
-        lx.tslot = site++;
+        set_tslot(lx, site++);
         if (!plan->ops->o2(136, plan->sq, 1, Launch{dim3(nimg * g.L * std::max(1, plan->o2x_lay[j1].nsplit)),
                                              dim3(plan->o2x_threads[j1]), plan->o2x_lds[j1], stream},
                            plan->dp, lx, j1, nimg, img0, hexp, d_out, pooled, j1 + 1))
@@ -1321,7 +1323,7 @@ int resident_level(const wst_plan* plan, int j1, int nimg, long long img0, unsig
         return timer.end(stream, 1 + g.J + j1);
     }
     LdsLayout lay2 = plan->o2_lay[j1];
-    lay2.tslot = site++;
+    set_tslot(lay2, site++);
     if (!plan->ops->o2(plan->cap[j1], plan->sq, 0,
                        Launch{dim3(nimg * g.L), dim3(plan->o2_threads[j1]), plan->o2_lds[j1], stream},
                        plan->dp, lay2, j1, nimg, img0, hexp, d_out, pooled, j1 + 1))
@@ -1481,7 +1483,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         const int j2f = plan->hg_j2first[j1];
         if (j2f < J) {
             LdsLayout lh = plan->hg_lay[j1];
-            lh.tslot = site++;
+            set_tslot(lh, site++);
             if (!plan->ops->o2(136, 1, 1, Launch{dim3(nimg * L * std::max(1, plan->hg_lay[j1].nsplit)),
                                                  dim3(plan->hg_threads[j1]), plan->hg_lds[j1], stream},
                                dp, lh, j1, nimg, img0, hbig, d_out, pooled, j2f))
@@ -1595,7 +1597,7 @@ int forward_impl(const wst_plan* plan, const float* d_in, int64_t nbatch, float*
         }
         if ((rc = timer.begin(stream)) != WST_OK) return rc;
         LdsLayout lp = plan->prep_lay;
-        lp.tslot = site++;
+        set_tslot(lp, site++);
         plan->ops->prep(Launch{dim3(nimg), dim3(plan->prep_threads), plan->prep_lds, stream},
                         plan->dp, lp, d_in + c0 * inM * inN, img0, xhat, d_out, pooled);
         WST_HIP_CHECK(hipGetLastError());

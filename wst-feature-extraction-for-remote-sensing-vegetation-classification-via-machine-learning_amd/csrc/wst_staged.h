@@ -433,7 +433,9 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
     }
     // kColModLp / kColModLpFwd: |.| * scale in place (.x), then partials over the rows of each
     // column (and, Fwd, the column spectra of U)
-    __shared__ float csum_t[C];   // kColModLpFwd: this tile's column sums
+    // kColModLpFwd: this tile's column sums, in the dynamic LDS after the tile and its taps (a
+    // static array would leave less than the 160 KiB the launch may request)
+    float* csum_t = reinterpret_cast<float*>(A + C * ld) + (a.g_lds ? n * a.oms : 0);
     wstdev::EpiModulus mod{a.scale, 0.f};
     big_fft<N, INV>(A, wstfft::Lines(1, 0, nc, ld, 1), n, tw, mod);
     // V[q][a] = sum_p GMnat[p][a] m[p][q] (a < oM) and the column sum: the taps are staged in LDS
