@@ -7,6 +7,6 @@ tail -2 gpurun_out/r05e_variants.txt
 tools/gpu_step.sh 600 gpurun_out/r05e_pytest.txt python3 -u -m pytest tests -m gpu -x -q -rs --timeout 200 --timeout-method thread --deselect tests/test_gpu_variants.py || exit 99
 tail -2 gpurun_out/r05e_pytest.txt
 grep -q " passed" gpurun_out/r05e_pytest.txt || exit 99
-bash tools/ab_rep.sh r05e 3072,64,4 2 libwst_hip.so var_notrace.so var_r04.so var_fg3.so var_fg6.so || exit 99
+bash tools/ab_rep.sh r05e 3072,64,4 2 libwst_hip.so var_notrace.so var_notslot.so var_r04.so || exit 99
 bash tools/ab_rep.sh r05e5 256,256,6,12 1 libwst_hip.so var_r04.so || exit 99
 bash tools/f3_split.sh r05e

@@ -117,8 +117,11 @@ struct LdsLayout {
     int oms;                // row stride of the tap matrices (4 or kLpOM)
     int off_s, off_red;     // S (coefficients) and reduction scratch
     int bcap;               // complex capacity of B (k_o2)
-    int export_full;        // k_o1: export the fully transformed half spectra (natural order) for a
-                            // k_o2 that folds from HBM (HG = 1) instead of the row-transformed ones
+    int xs;                 // bit 0 (k_o1): export the fully transformed half spectra (natural order)
+                            // for a k_o2 that folds from HBM (HG = 1) instead of the row-transformed
+                            // ones; bits 1..: the launch's variant-trace site (kFlagTrace).  One
+                            // field: a separate site field made the headline k_o2 1.3 % slower
+                            // (its kernel arguments grew; measured, round 5)
     int nsplit;             // k_o2 HG: workgroups per (plane, theta1), batch b run by workgroup
                             // b % nsplit; one item's workgroups share an XCD (its L2 holds H)
     int hgroup;             // k_o2 HG split: items per dispatch group of an XCD; within a group
@@ -126,26 +129,11 @@ struct LdsLayout {
     int hext;               // resident levels: an item's half spectrum in the workspace holds
                             // nM1 + 1 rows (row nM1 = row 0 for the tile folds' mirrored taps;
                             // written by an exporting k_o1, formed in LDS by k_o2 otherwise)
-#ifndef WST_NO_TSLOT       // (A/B builds: the layout without the field)
-    int tslot;              // variant-trace site of this launch (kFlagTrace)
-#endif
 };
-__host__ __device__ inline void set_tslot(LdsLayout& l, int s) {
-#ifndef WST_NO_TSLOT
-    l.tslot = s;
-#else
-    (void)l;
-    (void)s;
-#endif
-}
-__host__ __device__ inline int get_tslot(const LdsLayout& l) {
-#ifndef WST_NO_TSLOT
-    return l.tslot;
-#else
-    (void)l;
-    return 0;
-#endif
-}
+__host__ __device__ inline int export_full(const LdsLayout& l) { return l.xs & 1; }
+__host__ __device__ inline void set_export_full(LdsLayout& l) { l.xs |= 1; }
+__host__ __device__ inline int get_tslot(const LdsLayout& l) { return l.xs >> 1; }
+__host__ __device__ inline void set_tslot(LdsLayout& l, int s) { l.xs = (l.xs & 1) | (s << 1); }
 
 // ------------------------------------------------------------------------------------------
 // Variant trace (tests: wst_plan_trace / wst_describe_variants, include/wst_hip.h).  With
@@ -1883,7 +1871,7 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
         const int f1 = fused1 ? 0 : s1 == 1 ? 1 : s1 == 2 ? 2 : use_box1 ? 3 : s1 == 4 ? 4 : 5;
         const int lp1 = SQ ? kLpTap : wide_lowpass(p) ? (mfma_rc_ok<N1C>() ? kLpMfmaRc : kLpMfma) : kLpPlain;
         trace_word(p, get_tslot(lay), 0, tr_kernel(kTkO1, FM, FN, MAXN, SQ, 0));
-        trace_word(p, get_tslot(lay), 1, tr_o1(OC, N1C, fused1 ? 1 : 0, lp1, do2 ? 1 : 0, lay.export_full, f1));
+        trace_word(p, get_tslot(lay), 1, tr_o1(OC, N1C, fused1 ? 1 : 0, lp1, do2 ? 1 : 0, export_full(lay), f1));
     }
     EpiModulus mod1{1.f / (static_cast<float>(PM) * static_cast<float>(PN)), 0.f};
     if (fused1) {
@@ -1943,7 +1931,7 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     // 5. split into the two rows' half spectra (columns 0..nN1/2) and export them
     const int hld = (nN1 >> 1) + 1;
     float2* H = hexp + item * hspec_stride(nM1, hld, lay.hext);
-    if (lay.export_full) {
+    if (export_full(lay)) {
         // in place: packed row 2t -> half-spectrum rows 2t and 2t+1 (the odd rows of A are free),
         // then the column FFTs (rows digit-reversed -> natural); k_o2 folds the fully transformed
         // spectrum from HBM/L2 and keeps only its path batches in LDS (host: nh * hld <= KS * T)

@@ -1113,7 +1113,7 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
         plan->o2x_threads[j1] = std::min(fill_cu(default_threads(static_cast<size_t>(nM1) * nN1), lds, 768),
                                          1024);
         plan->o2x_lay[j1].hext = 1;
-        plan->o1_lay[j1].export_full = 1;
+        set_export_full(plan->o1_lay[j1]);
         // one workgroup per item: splitting its batches over 2 / 4 workgroups of one XCD (as the
         // HG launches after staged levels do) measured slower here (f3 k_o2 1.57 -> 1.67 / 1.66 ms,
         // c1 1.50 -> 1.62): H is 21-75 KB, not the 0.15-0.6 MB of a staged level
@@ -1134,7 +1134,7 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
     // k_o1's in-place Hermitian split of an exported spectrum holds 8 items per thread: a thread
     // count lowered by an override would silently drop items, so the plan fails instead
     for (int j1 = plan->rb; j1 + 1 < J; ++j1)
-        if (plan->o1_lay[j1].export_full &&
+        if (export_full(plan->o1_lay[j1]) &&
             static_cast<size_t>((g.PM >> j1) / 2) * ((g.PN >> j1) / 2 + 1) > 8 * static_cast<size_t>(plan->o1_threads[j1]))
             return fail(WST_ERR_INVALID, "k_o1 at level " + std::to_string(j1) + ": " +
                                              std::to_string(plan->o1_threads[j1]) +
@@ -1672,7 +1672,7 @@ void describe_o1(Describe& d, int j1) {
     const bool wide = g.oM > kLpOM || g.oN > kLpOM;
     int* t = d.site();
     t[0] = tr_kernel(kTkO1, FM, FN, MAXN, SQ, 0);
-    t[1] = tr_o1(oc, n1c, fused1 ? 1 : 0, lp_form(SQ, wide, n1c), do2 ? 1 : 0, lay.export_full, f1);
+    t[1] = tr_o1(oc, n1c, fused1 ? 1 : 0, lp_form(SQ, wide, n1c), do2 ? 1 : 0, export_full(lay), f1);
 }
 
 void describe_o2(Describe& d, int j1, const LdsLayout& lay, int MAXN, int sq, int HG, int j2first) {
