@@ -154,7 +154,9 @@ int wst_forward_profiled(const wst_plan* plan, const float* d_in, int64_t nbatch
  *   wst_describe_variants : the same for a geometry, without a GPU (a host-only plan: no
  *                           device allocation, zero-valued filters of the right shapes).
  *   wst_plan_trace        : enable (1) / disable (0) the device trace: every later forward's
- *                           launches record the words they actually ran.
+ *                           launches record the words they actually ran.  Only in the trace build
+ *                           (libwst_hip_trace.so = the same sources with -DWST_TRACE); the product
+ *                           library has no trace code and returns WST_ERR_UNSUPPORTED for enable.
  *   wst_plan_read_trace   : copy the device trace (synchronises the device); *nwords = the
  *                           plan's site count x 12.
  * out may be NULL for a size query in the first two (then only *nwords is set).

@@ -2,9 +2,10 @@
 which variant it ran (tests/test_variants_cpu.py proves the cover reaches them all).
 
 For each geometry of tests/variant_geometries.py: one uint8/255 plane (regenerated from its seed)
-through a plan with the device trace on (wst_plan_trace), then
-  * the trace words the kernels wrote == the host mirror's prediction (wst_plan_variants);
-  * the coefficients at the fixture's sampled positions (all of them for maps <= 16 values)
+  * through the trace build (libwst_hip_trace.so: the same sources with -DWST_TRACE; the product
+    library carries no trace code) with the device trace on (wst_plan_trace): the words the
+    kernels wrote == the host mirror's prediction (wst_plan_variants);
+  * through the product library: the coefficients at the fixture's sampled positions (all of them for maps <= 16 values)
     meet the parity bar against the oracle's (tests/golden/variants_cover.npz,
     make_variant_golden.py): per coefficient max |d| / max |S_ref[k]| <= TOL, and elementwise on
     the significant entries (|S_ref| >= 1e-3 max |S_ref[k]|).
@@ -38,15 +39,25 @@ def test_variant_geometry_matches_oracle_and_mirror(i):
     g = tuple(int(v) for v in FIX["geoms"][i])
     assert g == tuple(COVER[i])
     M, N, J, L, mo = g
-    plan = _lib.Plan(M, N, J, L, mo, False)
-    plan.trace(True)
     x = torch.from_numpy(_plane(g)).cuda()
-    out = torch.empty((1, plan.K, plan.Mo, plan.No), device="cuda")
-    ws = torch.empty(plan.workspace_bytes(1), dtype=torch.uint8, device="cuda")
-    plan.forward(x.data_ptr(), 1, out.data_ptr(), False, ws.data_ptr(), ws.numel(),
-                 torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    dev, mirror = plan.read_trace(), plan.variants()
+
+    def run(plan):
+        out = torch.empty((1, plan.K, plan.Mo, plan.No), device="cuda")
+        ws = torch.empty(plan.workspace_bytes(1), dtype=torch.uint8, device="cuda")
+        plan.forward(x.data_ptr(), 1, out.data_ptr(), False, ws.data_ptr(), ws.numel(),
+                     torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        return out
+
+    plan = _lib.Plan(M, N, J, L, mo, False)                          # the product library
+    out = run(plan)
+    tplan = _lib.Plan(M, N, J, L, mo, False, lib=_lib.load_trace())   # the trace build
+    tplan.trace(True)
+    tout = run(tplan)
+    dev, mirror = tplan.read_trace(), plan.variants()
+    assert np.array_equal(tplan.variants(), mirror)
+    # the trace build computes what the product computes (its trace stores are the only difference)
+    assert torch.equal(out, tout), f"{g}: trace build and product differ"
     if not np.array_equal(dev, mirror):
         bad = [s for s in range(len(mirror)) if not np.array_equal(dev[s], mirror[s])]
         raise AssertionError(f"{g}: device ran another variant than the mirror predicts at sites {bad[:4]}: "
@@ -62,4 +73,11 @@ def test_variant_geometry_matches_oracle_and_mirror(i):
     sig = np.abs(ref) >= SIGNIFICANT * scale[:, None]
     ew = np.where(sig & (ref != 0), np.abs(got - ref) / np.where(ref != 0, np.abs(ref), 1.0), 0.0)
     assert ew.max() <= TOL, f"{g}: elementwise rel err {ew.max():.3e} on significant entries"
-    plan.trace(False)
+    tplan.trace(False)
+
+
+def test_product_library_has_no_trace_code():
+    """wst_plan_trace is refused by the product library: its kernels carry no trace stores."""
+    plan = _lib.Plan(64, 64, 4, 8)
+    with pytest.raises(_lib.WSTError):
+        plan.trace(True)

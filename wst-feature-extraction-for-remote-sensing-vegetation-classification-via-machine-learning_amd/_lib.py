@@ -78,6 +78,10 @@ class WSTError(RuntimeError):
         self.code = code
 
 
+TRACE_LIB_NAME = "libwst_hip_trace.so"   # the same sources with -DWST_TRACE (tests only)
+_trace_lib = None
+
+
 def load() -> ctypes.CDLL:
     """Load (once) and type the library.  Raises RuntimeError if it was not built."""
     global _lib
@@ -86,92 +90,107 @@ def load() -> ctypes.CDLL:
     with _lock:
         if _lib is not None:
             return _lib
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(
-                f"{LIB_NAME} not found at {LIB_PATH}: the HIP extension is not built "
-                "(run `python -c 'import __graft_entry__ as g; g.build()'` or `make -C <pkg>/csrc`)")
-        lib = ctypes.CDLL(LIB_PATH)
-        c_int, c_i64, c_vp, c_sz = ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t
-        lib.wst_abi_version.restype = c_int
-        lib.wst_abi_version.argtypes = []
-        lib.wst_last_error.restype = ctypes.c_char_p
-        lib.wst_last_error.argtypes = []
-        lib.wst_plan_create.restype = c_int
-        lib.wst_plan_create.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int,
-                                        ctypes.POINTER(c_vp)]
-        conv_p = ctypes.POINTER(Convention)
-        lib.wst_default_convention.restype = c_int
-        lib.wst_default_convention.argtypes = [conv_p]
-        lib.wst_plan_create_ex.restype = c_int
-        lib.wst_plan_create_ex.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, conv_p,
-                                           ctypes.POINTER(c_vp)]
-        lib.wst_host_filter_ex.restype = c_int
-        lib.wst_host_filter_ex.argtypes = [c_int] * 8 + [conv_p, ctypes.POINTER(ctypes.c_double),
-                                                         c_i64]
-        lib.wst_plan_destroy.restype = c_int
-        lib.wst_plan_destroy.argtypes = [c_vp]
-        lib.wst_output_shape.restype = c_int
-        lib.wst_output_shape.argtypes = [c_vp] + [ctypes.POINTER(c_int)] * 3
-        lib.wst_padded_shape.restype = c_int
-        lib.wst_padded_shape.argtypes = [c_vp] + [ctypes.POINTER(c_int)] * 2
-        lib.wst_workspace_bytes.restype = c_int
-        lib.wst_workspace_bytes.argtypes = [c_vp, c_i64, ctypes.POINTER(c_sz)]
-        u8p, f64p, i32p = ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p
-        lib.wst_salt_pepper_counts.restype = c_int
-        lib.wst_salt_pepper_counts.argtypes = [c_int, c_int, c_int, ctypes.c_double,
-                                               ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]
-        lib.wst_noise_apply.restype = c_int
-        lib.wst_noise_apply.argtypes = [c_int, ctypes.c_double, u8p, c_i64, c_int, c_int, c_int,
-                                        f64p, i32p, i32p, c_int, c_vp, c_vp]
-        lib.wst_noise_generate.restype = c_int
-        lib.wst_noise_generate.argtypes = [c_int, ctypes.c_double, u8p, c_i64, c_int, c_int, c_int,
-                                           ctypes.c_uint64, c_int, c_vp, c_vp]
-        lib.wst_advanced_stats.restype = c_int
-        lib.wst_advanced_stats.argtypes = [c_vp, c_i64, c_int, c_int, c_vp, c_vp]
-        lib.wst_patch_generate.restype = c_int
-        lib.wst_patch_generate.argtypes = [ctypes.c_uint64, c_i64, c_i64, c_int, c_int, c_int, c_int,
-                                           c_vp, c_vp]
-        lib.wst_u8_to_chw.restype = c_int
-        lib.wst_u8_to_chw.argtypes = [c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp]
-        lib.wst_probe_copy.restype = c_int
-        lib.wst_probe_copy.argtypes = [c_vp, c_vp, c_sz, c_vp]
-        lib.wst_probe_fma.restype = c_int
-        lib.wst_probe_fma.argtypes = [c_vp, c_i64, c_int, c_vp]
-        lib.wst_aux_last_error.restype = ctypes.c_char_p
-        lib.wst_aux_last_error.argtypes = []
-        lib.wst_preferred_batch.restype = c_int
-        lib.wst_preferred_batch.argtypes = [c_vp, ctypes.POINTER(c_i64)]
-        lib.wst_plan_staging.restype = c_int
-        lib.wst_plan_staging.argtypes = [c_vp] + [ctypes.POINTER(c_int)] * 3
-        lib.wst_internal_workspaces.restype = c_int
-        lib.wst_internal_workspaces.argtypes = [c_vp, ctypes.POINTER(c_int), ctypes.POINTER(c_sz)]
-        lib.wst_forward.restype = c_int
-        lib.wst_forward.argtypes = [c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_sz, c_vp]
-        lib.wst_forward_profiled.restype = c_int
-        lib.wst_forward_profiled.argtypes = [c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_sz, c_vp,
-                                             ctypes.POINTER(ctypes.c_float), c_int]
-        lib.wst_host_filter.restype = c_int
-        lib.wst_host_filter.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
-                                        ctypes.POINTER(ctypes.c_double), c_i64]
-        lib.wst_host_fft_lines.restype = c_int
-        lib.wst_host_fft_lines.argtypes = [c_int, c_int, c_int, c_vp] + [c_int] * 6 + [c_vp]
-        i64p = ctypes.POINTER(c_i64)
-        # (an older A/B build chosen by use_library may lack the introspection entry points;
-        # tests/test_abi.py checks the product library exports all of EXPORTS)
-        if hasattr(lib, "wst_plan_variants"):
-            lib.wst_plan_variants.restype = c_int
-            lib.wst_plan_variants.argtypes = [c_vp, c_vp, c_i64, i64p]
-            lib.wst_describe_variants.restype = c_int
-            lib.wst_describe_variants.argtypes = [c_int] * 5 + [c_vp, c_i64, i64p]
-            lib.wst_plan_trace.restype = c_int
-            lib.wst_plan_trace.argtypes = [c_vp, c_int]
-            lib.wst_plan_read_trace.restype = c_int
-            lib.wst_plan_read_trace.argtypes = [c_vp, c_vp, c_i64, i64p]
-        v = lib.wst_abi_version()
-        if v != ABI_VERSION:
-            raise RuntimeError(f"{LIB_NAME} ABI version {v} != expected {ABI_VERSION}; rebuild it")
-        _lib = lib
-        return lib
+        _lib = _open(LIB_PATH, LIB_NAME)
+        return _lib
+
+
+def load_trace() -> ctypes.CDLL:
+    """The variant-trace build (tests/test_gpu_variants.py): kernels that record which body and
+    level branches they ran (wst_plan_trace); the product library carries no trace code."""
+    global _trace_lib
+    with _lock:
+        if _trace_lib is None:
+            _trace_lib = _open(os.path.join(PKG_DIR, TRACE_LIB_NAME), TRACE_LIB_NAME)
+        return _trace_lib
+
+
+def _open(path, name) -> ctypes.CDLL:
+    """Open and type one build of the library."""
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"{name} not found at {path}: the HIP extension is not built "
+            "(run `python -c 'import __graft_entry__ as g; g.build()'` or `make -C <pkg>/csrc`)")
+    lib = ctypes.CDLL(path)
+    c_int, c_i64, c_vp, c_sz = ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t
+    lib.wst_abi_version.restype = c_int
+    lib.wst_abi_version.argtypes = []
+    lib.wst_last_error.restype = ctypes.c_char_p
+    lib.wst_last_error.argtypes = []
+    lib.wst_plan_create.restype = c_int
+    lib.wst_plan_create.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int,
+                                    ctypes.POINTER(c_vp)]
+    conv_p = ctypes.POINTER(Convention)
+    lib.wst_default_convention.restype = c_int
+    lib.wst_default_convention.argtypes = [conv_p]
+    lib.wst_plan_create_ex.restype = c_int
+    lib.wst_plan_create_ex.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, conv_p,
+                                       ctypes.POINTER(c_vp)]
+    lib.wst_host_filter_ex.restype = c_int
+    lib.wst_host_filter_ex.argtypes = [c_int] * 8 + [conv_p, ctypes.POINTER(ctypes.c_double),
+                                                     c_i64]
+    lib.wst_plan_destroy.restype = c_int
+    lib.wst_plan_destroy.argtypes = [c_vp]
+    lib.wst_output_shape.restype = c_int
+    lib.wst_output_shape.argtypes = [c_vp] + [ctypes.POINTER(c_int)] * 3
+    lib.wst_padded_shape.restype = c_int
+    lib.wst_padded_shape.argtypes = [c_vp] + [ctypes.POINTER(c_int)] * 2
+    lib.wst_workspace_bytes.restype = c_int
+    lib.wst_workspace_bytes.argtypes = [c_vp, c_i64, ctypes.POINTER(c_sz)]
+    u8p, f64p, i32p = ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p
+    lib.wst_salt_pepper_counts.restype = c_int
+    lib.wst_salt_pepper_counts.argtypes = [c_int, c_int, c_int, ctypes.c_double,
+                                           ctypes.POINTER(c_i64), ctypes.POINTER(c_i64)]
+    lib.wst_noise_apply.restype = c_int
+    lib.wst_noise_apply.argtypes = [c_int, ctypes.c_double, u8p, c_i64, c_int, c_int, c_int,
+                                    f64p, i32p, i32p, c_int, c_vp, c_vp]
+    lib.wst_noise_generate.restype = c_int
+    lib.wst_noise_generate.argtypes = [c_int, ctypes.c_double, u8p, c_i64, c_int, c_int, c_int,
+                                       ctypes.c_uint64, c_int, c_vp, c_vp]
+    lib.wst_advanced_stats.restype = c_int
+    lib.wst_advanced_stats.argtypes = [c_vp, c_i64, c_int, c_int, c_vp, c_vp]
+    lib.wst_patch_generate.restype = c_int
+    lib.wst_patch_generate.argtypes = [ctypes.c_uint64, c_i64, c_i64, c_int, c_int, c_int, c_int,
+                                       c_vp, c_vp]
+    lib.wst_u8_to_chw.restype = c_int
+    lib.wst_u8_to_chw.argtypes = [c_vp, c_i64, c_int, c_int, c_int, c_vp, c_vp]
+    lib.wst_probe_copy.restype = c_int
+    lib.wst_probe_copy.argtypes = [c_vp, c_vp, c_sz, c_vp]
+    lib.wst_probe_fma.restype = c_int
+    lib.wst_probe_fma.argtypes = [c_vp, c_i64, c_int, c_vp]
+    lib.wst_aux_last_error.restype = ctypes.c_char_p
+    lib.wst_aux_last_error.argtypes = []
+    lib.wst_preferred_batch.restype = c_int
+    lib.wst_preferred_batch.argtypes = [c_vp, ctypes.POINTER(c_i64)]
+    lib.wst_plan_staging.restype = c_int
+    lib.wst_plan_staging.argtypes = [c_vp] + [ctypes.POINTER(c_int)] * 3
+    lib.wst_internal_workspaces.restype = c_int
+    lib.wst_internal_workspaces.argtypes = [c_vp, ctypes.POINTER(c_int), ctypes.POINTER(c_sz)]
+    lib.wst_forward.restype = c_int
+    lib.wst_forward.argtypes = [c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_sz, c_vp]
+    lib.wst_forward_profiled.restype = c_int
+    lib.wst_forward_profiled.argtypes = [c_vp, c_vp, c_i64, c_vp, c_int, c_vp, c_sz, c_vp,
+                                         ctypes.POINTER(ctypes.c_float), c_int]
+    lib.wst_host_filter.restype = c_int
+    lib.wst_host_filter.argtypes = [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    ctypes.POINTER(ctypes.c_double), c_i64]
+    lib.wst_host_fft_lines.restype = c_int
+    lib.wst_host_fft_lines.argtypes = [c_int, c_int, c_int, c_vp] + [c_int] * 6 + [c_vp]
+    i64p = ctypes.POINTER(c_i64)
+    # (an older A/B build chosen by use_library may lack the introspection entry points;
+    # tests/test_abi.py checks the product library exports all of EXPORTS)
+    if hasattr(lib, "wst_plan_variants"):
+        lib.wst_plan_variants.restype = c_int
+        lib.wst_plan_variants.argtypes = [c_vp, c_vp, c_i64, i64p]
+        lib.wst_describe_variants.restype = c_int
+        lib.wst_describe_variants.argtypes = [c_int] * 5 + [c_vp, c_i64, i64p]
+        lib.wst_plan_trace.restype = c_int
+        lib.wst_plan_trace.argtypes = [c_vp, c_int]
+        lib.wst_plan_read_trace.restype = c_int
+        lib.wst_plan_read_trace.argtypes = [c_vp, c_vp, c_i64, i64p]
+    v = lib.wst_abi_version()
+    if v != ABI_VERSION:
+        raise RuntimeError(f"{name} ABI version {v} != expected {ABI_VERSION}; rebuild it")
+    return lib
 
 
 def last_error() -> str:
@@ -236,18 +255,24 @@ def host_fft_lines(data: np.ndarray, n, inverse, nb, bs, nl, ls, es, threads=256
 class Plan:
     """Owning handle of a ``wst_plan`` (bound to the device current at creation)."""
 
-    def __init__(self, M, N, J, L, max_order=2, pre_pad=False, convention=None):
-        lib = load()
+    def __init__(self, M, N, J, L, max_order=2, pre_pad=False, convention=None, lib=None):
+        lib = lib or load()
+        self._L = lib
         h = ctypes.c_void_p()
-        check(lib.wst_plan_create_ex(int(M), int(N), int(J), int(L), int(max_order),
+        self._chk(lib.wst_plan_create_ex(int(M), int(N), int(J), int(L), int(max_order),
                                      1 if pre_pad else 0, _conv_ptr(convention), ctypes.byref(h)))
         self._h = h
         K, Mo, No = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        check(lib.wst_output_shape(h, ctypes.byref(K), ctypes.byref(Mo), ctypes.byref(No)))
+        self._chk(lib.wst_output_shape(h, ctypes.byref(K), ctypes.byref(Mo), ctypes.byref(No)))
         self.K, self.Mo, self.No = K.value, Mo.value, No.value
         PM, PN = ctypes.c_int(), ctypes.c_int()
-        check(lib.wst_padded_shape(h, ctypes.byref(PM), ctypes.byref(PN)))
+        self._chk(lib.wst_padded_shape(h, ctypes.byref(PM), ctypes.byref(PN)))
         self.PM, self.PN = PM.value, PN.value
+
+    def _chk(self, code: int) -> None:
+        """Status check against this plan's library (its thread-local last error)."""
+        if code != WST_OK:
+            raise WSTError(code, self._L.wst_last_error().decode(errors="replace") or f"wst status {code}")
 
     @property
     def handle(self):
@@ -255,30 +280,30 @@ class Plan:
 
     def workspace_bytes(self, nbatch: int) -> int:
         b = ctypes.c_size_t()
-        check(load().wst_workspace_bytes(self._h, int(nbatch), ctypes.byref(b)))
+        self._chk(self._L.wst_workspace_bytes(self._h, int(nbatch), ctypes.byref(b)))
         return b.value
 
     def preferred_batch(self) -> int:
         """Planes per workspace chunk (wst_preferred_batch)."""
         b = ctypes.c_int64()
-        check(load().wst_preferred_batch(self._h, ctypes.byref(b)))
+        self._chk(self._L.wst_preferred_batch(self._h, ctypes.byref(b)))
         return b.value
 
     def staging(self):
         """(rb, nst, sq) of the plan's level schedule (wst_plan_staging)."""
         rb, nst, sq = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        check(load().wst_plan_staging(self._h, ctypes.byref(rb), ctypes.byref(nst), ctypes.byref(sq)))
+        self._chk(self._L.wst_plan_staging(self._h, ctypes.byref(rb), ctypes.byref(nst), ctypes.byref(sq)))
         return rb.value, nst.value, sq.value
 
     def internal_workspaces(self):
         """(count, bytes) of the per-stream internal workspaces (wst_internal_workspaces)."""
         n, b = ctypes.c_int(), ctypes.c_size_t()
-        check(load().wst_internal_workspaces(self._h, ctypes.byref(n), ctypes.byref(b)))
+        self._chk(self._L.wst_internal_workspaces(self._h, ctypes.byref(n), ctypes.byref(b)))
         return n.value, b.value
 
     def forward(self, d_in: int, nbatch: int, d_out: int, pooled: bool, d_ws: int, ws_bytes: int,
                 stream: int) -> None:
-        check(load().wst_forward(self._h, ctypes.c_void_p(d_in), int(nbatch),
+        self._chk(self._L.wst_forward(self._h, ctypes.c_void_p(d_in), int(nbatch),
                                  ctypes.c_void_p(d_out), 1 if pooled else 0,
                                  ctypes.c_void_p(d_ws or None), int(ws_bytes),
                                  ctypes.c_void_p(stream or None)))
@@ -287,7 +312,7 @@ class Plan:
                          ws_bytes: int, stream: int, nslots: int):
         """wst_forward_profiled: returns per-kernel summed milliseconds (list of nslots)."""
         ms = (ctypes.c_float * nslots)()
-        check(load().wst_forward_profiled(self._h, ctypes.c_void_p(d_in), int(nbatch),
+        self._chk(self._L.wst_forward_profiled(self._h, ctypes.c_void_p(d_in), int(nbatch),
                                           ctypes.c_void_p(d_out), 1 if pooled else 0,
                                           ctypes.c_void_p(d_ws or None), int(ws_bytes),
                                           ctypes.c_void_p(stream or None), ms, nslots))
@@ -296,26 +321,26 @@ class Plan:
     def variants(self) -> np.ndarray:
         """Host-mirror trace words of one chunk (sites x 12, wst_plan_variants)."""
         n = ctypes.c_int64()
-        check(load().wst_plan_variants(self._h, None, 0, ctypes.byref(n)))
+        self._chk(self._L.wst_plan_variants(self._h, None, 0, ctypes.byref(n)))
         out = np.zeros(max(n.value, 1), np.int32)
-        check(load().wst_plan_variants(self._h, out.ctypes.data, out.size, ctypes.byref(n)))
+        self._chk(self._L.wst_plan_variants(self._h, out.ctypes.data, out.size, ctypes.byref(n)))
         return out[:n.value].reshape(-1, 12)
 
     def trace(self, enable: bool) -> None:
         """Enable / disable the device variant trace (wst_plan_trace)."""
-        check(load().wst_plan_trace(self._h, 1 if enable else 0))
+        self._chk(self._L.wst_plan_trace(self._h, 1 if enable else 0))
 
     def read_trace(self) -> np.ndarray:
         """Device trace words of the last traced forward (sites x 12, wst_plan_read_trace)."""
         n = ctypes.c_int64()
-        check(load().wst_plan_variants(self._h, None, 0, ctypes.byref(n)))
+        self._chk(self._L.wst_plan_variants(self._h, None, 0, ctypes.byref(n)))
         out = np.zeros(max(n.value, 1), np.int32)
-        check(load().wst_plan_read_trace(self._h, out.ctypes.data, out.size, ctypes.byref(n)))
+        self._chk(self._L.wst_plan_read_trace(self._h, out.ctypes.data, out.size, ctypes.byref(n)))
         return out[:n.value].reshape(-1, 12)
 
     def close(self):
-        if getattr(self, "_h", None) is not None and _lib is not None:
-            _lib.wst_plan_destroy(self._h)
+        if getattr(self, "_h", None) is not None and getattr(self, "_L", None) is not None:
+            self._L.wst_plan_destroy(self._h)
             self._h = None
 
     def __del__(self):

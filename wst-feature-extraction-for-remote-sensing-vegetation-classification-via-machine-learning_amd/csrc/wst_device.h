@@ -190,9 +190,13 @@ constexpr int tr_big(int mode, int fold_all, int fold1, int box, int wide, int g
 }
 // The writer of a site: lane 0 of workgroup 0, only while tracing.  Callers wrap the whole
 // word computation in `if (tracing(p, tslot))` so a production launch (kFlagTrace clear) skips
-// it with one uniform branch and the hot code around it is laid out as without it.
+// it with one uniform branch.  Compiled in only with -DWST_TRACE (libwst_hip_trace.so, the tests'
+// build): any trace code in the product kernels cost 1-2.5 % (measured, round 5).
 __device__ __forceinline__ bool tracing(const DevParams& p, int tslot) {
-#ifdef WST_NO_TRACE   // A/B builds only (tools/variant.sh)
+#ifndef WST_TRACE   // product library: no trace code at all (any form of it measured 1-2.5 % on the
+                    // headline kernels); libwst_hip_trace.so is the same sources with -DWST_TRACE
+    (void)p;
+    (void)tslot;
     return false;
 #endif
     return (p.flags & kFlagTrace) && tslot >= 0 && tslot < kTraceSites && threadIdx.x == 0 &&
@@ -1752,10 +1756,6 @@ __device__ __forceinline__ void prep_body(unsigned char* smem, const DevParams& 
     const long long img = img0 + local;
     const int inM = p.pre_pad ? PM : p.M, inN = p.pre_pad ? PN : p.N;
     const float* x = in + local * inM * inN;
-    if (tracing(p, get_tslot(lay))) {
-        trace_word(p, get_tslot(lay), 0, tr_kernel(kTkPrep, FM, FN, 0, 0, 0));
-        trace_word(p, get_tslot(lay), 1, tr_prep(PC, wide_lowpass(p) ? (mfma_rc_ok<PC>() ? kLpMfmaRc : kLpMfma) : kLpPlain));
-    }
     float part = 0.f;
     for (GridIter it(PN); it.u < PM; it.next()) {
         const int su = p.pre_pad ? it.u : reflect_index(it.u - p.padTop, p.M);
@@ -1788,6 +1788,10 @@ __device__ __forceinline__ void prep_body(unsigned char* smem, const DevParams& 
     lds_fft2<FM, FN, 0, wstfft::kMaxFamilyN, kNat, false>(A, 1, 0, PM, PN, ld, tb.twM(0), tb.twN(0), id);
     float2* dst = xhat + local * n;
     for (GridIter it(PN); it.u < PM; it.next()) dst[it.u * PN + it.v] = A[it.u * ld + it.v];
+    if (tracing(p, get_tslot(lay))) {   // (after the work: the body is laid out as without it)
+        trace_word(p, get_tslot(lay), 0, tr_kernel(kTkPrep, FM, FN, 0, 0, 0));
+        trace_word(p, get_tslot(lay), 1, tr_prep(PC, wide_lowpass(p) ? (mfma_rc_ok<PC>() ? kLpMfmaRc : kLpMfma) : kLpPlain));
+    }
 }
 
 // One workgroup per plane.  Square planes of the family's sizes in (48, 136] run with compile-time
@@ -1866,13 +1870,6 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     // 0.78 -> 0.79, so the exported-spectrum kernels keep the separate fold)
     constexpr bool FUSE1 = SQ && N1C >= kFuse1Min && wstfft::LineFFT<(N1C > 0 ? N1C : 2), true>::N2 > 1;
     const bool fused1 = FUSE1 && j1 == 0;
-    if (tracing(p, get_tslot(lay))) {
-        const int s1 = 1 << j1;
-        const int f1 = fused1 ? 0 : s1 == 1 ? 1 : s1 == 2 ? 2 : use_box1 ? 3 : s1 == 4 ? 4 : 5;
-        const int lp1 = SQ ? kLpTap : wide_lowpass(p) ? (mfma_rc_ok<N1C>() ? kLpMfmaRc : kLpMfma) : kLpPlain;
-        trace_word(p, get_tslot(lay), 0, tr_kernel(kTkO1, FM, FN, MAXN, SQ, 0));
-        trace_word(p, get_tslot(lay), 1, tr_o1(OC, N1C, fused1 ? 1 : 0, lp1, do2 ? 1 : 0, export_full(lay), f1));
-    }
     EpiModulus mod1{1.f / (static_cast<float>(PM) * static_cast<float>(PN)), 0.f};
     if (fused1) {
         if constexpr (FUSE1) {
@@ -1981,6 +1978,24 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     }
 }
 
+// Variant trace of a k_o1 body, written after it ran (so the body's code is laid out as without
+// it): the same compile-time constants and run-time tests the body's dispatch used.
+template <int FM, int FN, int MAXN, int SQ, int OC, int N1T = 0>
+__device__ __forceinline__ void trace_o1(const DevParams& p, const LdsLayout& lay, int j1) {
+    if (!tracing(p, get_tslot(lay))) return;
+    constexpr int N1C = N1T ? N1T : SQ ? unique_level(FM, MAXN) : 0;
+    constexpr bool FUSE1 = SQ && N1C >= kFuse1Min && wstfft::LineFFT<(N1C > 0 ? N1C : 2), true>::N2 > 1;
+    const bool fused1 = FUSE1 && j1 == 0;
+    const bool do2 = (p.max_order >= 2) && (j1 < p.J - 1);
+    const int b1 = p.box1_off[j1 * p.L + 0];   // workgroup 0 writes: item 0, theta1 = 0
+    const bool use_box1 = b1 >= 0 && (1 << j1) >= p.box1_min_s;
+    const int s1 = 1 << j1;
+    const int f1 = fused1 ? 0 : s1 == 1 ? 1 : s1 == 2 ? 2 : use_box1 ? 3 : s1 == 4 ? 4 : 5;
+    const int lp1 = SQ ? kLpTap : wide_lowpass(p) ? (mfma_rc_ok<N1C>() ? kLpMfmaRc : kLpMfma) : kLpPlain;
+    trace_word(p, get_tslot(lay), 0, tr_kernel(kTkO1, FM, FN, MAXN, SQ, 0));
+    trace_word(p, get_tslot(lay), 1, tr_o1(OC, N1C, fused1 ? 1 : 0, lp1, do2 ? 1 : 0, export_full(lay), f1));
+}
+
 template <int FM, int FN, int MAXN, int SQ>
 __global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevParams p, LdsLayout lay, int j1, int nimg,
                                              long long img0, const float2* __restrict__ xhat,
@@ -1991,6 +2006,7 @@ __global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevPara
     if constexpr (SQ && MAXN == 136) {
         if (p.oM == 4 && p.oN == 4 && lay.oms == 4) {
             k_o1_body<FM, FN, MAXN, SQ, 4>(smem, p, lay, j1, nimg, img0, xhat, hexp, out, pooled);
+            trace_o1<FM, FN, MAXN, SQ, 4>(p, lay, j1);
             return;
         }
     }
@@ -2004,6 +2020,7 @@ __global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevPara
                     if (!done && (p.PM >> j1) == N1X) {
                         done = true;
                         k_o1_body<FM, FN, MAXN, SQ, 0, N1X>(smem, p, lay, j1, nimg, img0, xhat, hexp, out, pooled);
+                        trace_o1<FM, FN, MAXN, SQ, 0, N1X>(p, lay, j1);
                     }
                 }
             });
@@ -2011,6 +2028,7 @@ __global__ void __launch_bounds__(1024, o1_min_waves(MAXN, FM, FN)) k_o1(DevPara
         }
     }
     k_o1_body<FM, FN, MAXN, SQ, 0>(smem, p, lay, j1, nimg, img0, xhat, hexp, out, pooled);
+    trace_o1<FM, FN, MAXN, SQ, 0>(p, lay, j1);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2282,8 +2300,11 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                       std::integral_constant<int, 0>{});
         }
     };
+    int br_run = 0;
+    dispatch(level, br_run);
     if (tracing(p, get_tslot(lay))) {
-        // trace pass: the same dispatch with a functor that only records each level's path
+        // trace pass, after the work (the hot code's layout and registers stay as without it):
+        // the same dispatch with a functor that only records each level's path
         constexpr int spec = HG ? 0 : (N1C > 0 && wstfft::LineFFT<(N1C > 0 ? N1C : 2), false>::N2 > 1) ? 1 : 2;
         int br = 0;
         const int lpw = wide_lowpass(p) ? 1 : 0;
@@ -2303,8 +2324,6 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
         trace_word(p, get_tslot(lay), 0, tr_kernel(kTkO2, FM, FN, MAXN, SQ, HG));
         trace_word(p, get_tslot(lay), 1, tr_o2(OC, LC, N1C, spec, br));
     }
-    int br_run = 0;
-    dispatch(level, br_run);
 }
 
 

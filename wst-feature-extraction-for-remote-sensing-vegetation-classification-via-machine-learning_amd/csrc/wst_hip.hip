@@ -1835,6 +1835,11 @@ int wst_describe_variants(int M, int N, int J, int L, int max_order, int32_t* ou
 int wst_plan_trace(wst_plan* plan, int enable) {
     if (!plan) return fail(WST_ERR_INVALID, "plan is NULL");
     if (plan->host_only) return fail(WST_ERR_INVALID, "host-only plan");
+#ifndef WST_TRACE
+    if (enable)
+        return fail(WST_ERR_UNSUPPORTED, "this library has no trace code: the variant trace is in "
+                                         "libwst_hip_trace.so (same sources, -DWST_TRACE)");
+#endif
     if (!enable) {
         plan->dp.flags &= ~kFlagTrace;
         return WST_OK;
