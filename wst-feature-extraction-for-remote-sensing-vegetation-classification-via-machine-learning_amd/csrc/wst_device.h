@@ -713,7 +713,7 @@ __device__ __forceinline__ void lds_lowpass_mfma(float2* U, int nb, int bs, int 
 // wave's column tile (nt = wave % nnt) for all of its (b, row-tile) tasks, step 2's operands are
 // issued at entry, behind step 1 -- instead of once per 8 K steps of every task (the L2 latency of
 // the tap loads, not the matrix pipe, bounded the phase).  Same operand order, K parts and results
-// as lds_lowpass_mfma.  Any wave count (see step 1).  Ends with a barrier.
+// as lds_lowpass_mfma.  Needs nw >= nnt (step 1; checked at plan creation).  Ends with a barrier.
 constexpr int mfma_k_steps(int k) {
     return 16 * (k / 64) + 4 * ((k % 64) / 16) + ((k % 16) + 3) / 4;
 }
@@ -772,13 +772,15 @@ __device__ __forceinline__ void lds_lowpass_mfma_rc(float2* U, int nb, int bs, i
         at2 = (t2_0 % (nat * nnt)) / nnt;
         load_ops(GM, nat, at2, g2);
     }
-    // 1. T = U GN: with nw >= nnt every wave keeps one column tile (waves w and w + nnt share
-    //    it, splitting its row tiles); with fewer waves than tiles a wave takes tiles w, w + nw, ...
-    const bool wide_wg = nw >= nnt;
-    for (int nt = wide_wg ? wave % nnt : wave; nt < nnt; nt += wide_wg ? nnt : nw) {
+    // 1. T = U GN: every wave keeps one column tile (waves w and w + nnt share it, splitting its
+    //    row tiles).  Needs nw >= nnt: the plan checks it for every launch that takes this form
+    //    (wst_hip.hip, rc_waves_ok); the max() only keeps a violating launch from spinning.  (A
+    //    nested loop serving nw < nnt here cost the f3 k_o2 1.8 %, measured round 5.)
+    {
         float g[KS];
+        const int nt = wave % nnt;
         load_ops(GN, nnt, nt, g);
-        for (int tk = wide_wg ? wave / nnt : 0; tk < nb * NMT; tk += wide_wg ? nw / nnt : 1) {
+        for (int tk = wave / nnt; tk < nb * NMT; tk += max(1, nw / nnt)) {
             const int b = tk / NMT, mt = tk - b * NMT;
             float2* Ub = U + b * bs;
             const int p = mt * 16 + li;

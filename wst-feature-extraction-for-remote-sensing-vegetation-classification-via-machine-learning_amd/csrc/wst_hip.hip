@@ -376,6 +376,7 @@ int cyclic_window(const std::vector<char>& hit) {
 int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
                 const wst_filter_convention* conv_in, bool device, wst_plan** out);
 std::vector<int> describe_chunk(const wst_plan* pl);
+bool rc_waves_ok(const wst_plan* pl, std::string& why);
 
 // C-ABI convention -> host struct (NULL = kymatio 0.3.0 as recalled); false on a bad value.
 bool to_convention(const wst_filter_convention* c, wst::FilterConvention& out) {
@@ -1143,6 +1144,8 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
     for (int j = 0; j < J; ++j) plan->box1_l0[j] = box1_off[static_cast<size_t>(j) * L];
     if (device) {
         // every k_o1 / k_o2 the plan launches must be one of the compiled instantiations
+        std::string why;
+        if (!rc_waves_ok(plan.get(), why)) return fail(WST_ERR_INVALID, why);
         const std::vector<int> w = describe_chunk(plan.get());
         for (size_t i = 0; i < w.size(); i += wstdev::kTraceW) {
             const int kind = w[i] >> 28, fm = (w[i] >> 22) & 63, fn = (w[i] >> 16) & 63, cap = (w[i] >> 4) & 4095;
@@ -1625,7 +1628,9 @@ int lp_form(bool sq, bool wide, int k) { return sq ? kLpTap : wide ? (rc_ok(k) ?
 struct Describe {
     const wst_plan* plan;
     std::vector<int> w;
-    int* site() {
+    std::vector<int> thr;   // workgroup size of each site
+    int* site(int threads) {
+        thr.push_back(threads);
         w.resize(w.size() + kTraceW, 0);
         return w.data() + w.size() - kTraceW;
     }
@@ -1642,7 +1647,7 @@ void describe_prep(Describe& d) {
             if (PC > 48 && PC <= 136 && g.PM == PC && g.PN == PC) pc = PC;
         }
     const bool wide = g.oM > kLpOM || g.oN > kLpOM;
-    int* t = d.site();
+    int* t = d.site(pl->prep_threads);
     t[0] = tr_kernel(kTkPrep, FM, FN, 0, 0, 0);
     t[1] = tr_prep(pc, wide ? (rc_ok(pc) ? kLpMfmaRc : kLpMfma) : kLpPlain);
 }
@@ -1670,12 +1675,13 @@ void describe_o1(Describe& d, int j1) {
     const bool box1 = pl->box1_l0[j1] >= 0 && s1 >= pl->dp.box1_min_s;
     const int f1 = fused1 ? 0 : s1 == 1 ? 1 : s1 == 2 ? 2 : box1 ? 3 : s1 == 4 ? 4 : 5;
     const bool wide = g.oM > kLpOM || g.oN > kLpOM;
-    int* t = d.site();
+    int* t = d.site(pl->o1_threads[j1]);
     t[0] = tr_kernel(kTkO1, FM, FN, MAXN, SQ, 0);
     t[1] = tr_o1(oc, n1c, fused1 ? 1 : 0, lp_form(SQ, wide, n1c), do2 ? 1 : 0, export_full(lay), f1);
 }
 
-void describe_o2(Describe& d, int j1, const LdsLayout& lay, int MAXN, int sq, int HG, int j2first) {
+void describe_o2(Describe& d, int j1, const LdsLayout& lay, int MAXN, int sq, int HG, int j2first,
+                 int threads) {
     const wst_plan* pl = d.plan;
     const wst::Geometry& g = pl->g;
     const int FM = pl->fam_m, FN = pl->fam_n, J = g.J, L = g.L, PM = g.PM, PN = g.PN;
@@ -1692,7 +1698,7 @@ void describe_o2(Describe& d, int j1, const LdsLayout& lay, int MAXN, int sq, in
     const int n1c = (SQ && !HG) ? unique_level(FM, MAXN) : 0;
     const int spec = HG ? 0 : (n1c > 0 && wstfft::split_n2(n1c) > 1) ? 1 : 2;
     const bool wide = g.oM > kLpOM || g.oN > kLpOM;
-    int* t = d.site();
+    int* t = d.site(threads);
     auto level = [&](int j2, int pb, int sc, int nc) {
         const int n1f = (SQ && nc > 0 && sc > 0) ? nc * sc : 0;
         const bool fuse = n1f > 0 && sc == 2 && n1f / 2 >= kFuseMin && wstfft::split_n2(n1f / 2) > 1;
@@ -1754,22 +1760,22 @@ void describe_o2(Describe& d, int j1, const LdsLayout& lay, int MAXN, int sq, in
 }
 
 void describe_big(Describe& d, bool rows, int n, bool inv, int body) {
-    int* t = d.site();
+    int* t = d.site(wstbig::kBigThreads);
     t[0] = tr_kernel(rows ? kTkBigRows : kTkBigCols, 0, 0, n, 0, inv ? 1 : 0);
     t[1] = body;
 }
 
 // One chunk's launch sites in forward_impl's order (staged_levels / resident_level).
-std::vector<int> describe_chunk(const wst_plan* pl) {
-    Describe d{pl, {}};
+Describe describe_sites(const wst_plan* pl) {
+    Describe d{pl, {}, {}};
     const wst::Geometry& g = pl->g;
     const int J = g.J, L = g.L;
     const int wide_maps = g.oM > 8 ? 1 : 0;
     auto resident = [&](int j1) {
         describe_o1(d, j1);
         if (!(g.max_order >= 2 && j1 < J - 1)) return;
-        if (pl->o2_export[j1]) describe_o2(d, j1, pl->o2x_lay[j1], 136, pl->sq, 1, j1 + 1);
-        else describe_o2(d, j1, pl->o2_lay[j1], pl->cap[j1], pl->sq, 0, j1 + 1);
+        if (pl->o2_export[j1]) describe_o2(d, j1, pl->o2x_lay[j1], 136, pl->sq, 1, j1 + 1, pl->o2x_threads[j1]);
+        else describe_o2(d, j1, pl->o2_lay[j1], pl->cap[j1], pl->sq, 0, j1 + 1, pl->o2_threads[j1]);
     };
     if (pl->rb > 0) {
         using namespace wstbig;
@@ -1793,14 +1799,36 @@ std::vector<int> describe_chunk(const wst_plan* pl) {
                 }
             }
             const int j2f = pl->hg_j2first[j1];
-            if (j2f < J) describe_o2(d, j1, pl->hg_lay[j1], 136, 1, 1, j2f);
+            if (j2f < J) describe_o2(d, j1, pl->hg_lay[j1], 136, 1, 1, j2f, pl->hg_threads[j1]);
         }
         for (int j1 = pl->rb; j1 < J; ++j1) resident(j1);
     } else {
         describe_prep(d);
         for (int j1 = 0; j1 < J; ++j1) resident(j1);
     }
-    return d.w;
+    return d;
+}
+std::vector<int> describe_chunk(const wst_plan* pl) { return describe_sites(pl).w; }
+
+// lds_lowpass_mfma_rc keeps one column tile per wave: every launch that takes it needs at least
+// oNp / 16 waves (true of every plan's default launch shapes; a thread override could break it)
+bool rc_waves_ok(const wst_plan* pl, std::string& why) {
+    const Describe d = describe_sites(pl);
+    const int nnt = ((pl->g.oN + 15) & ~15) >> 4;
+    for (size_t s = 0; s < d.thr.size(); ++s) {
+        const int* t = d.w.data() + s * kTraceW;
+        const int kind = t[0] >> 28;
+        bool rc = (kind == kTkPrep && ((t[1] >> 8) & 3) == kLpMfmaRc) ||
+                  (kind == kTkO1 && ((t[1] >> 13) & 3) == kLpMfmaRc);
+        if (kind == kTkO2)
+            for (int k = 2; k < kTraceW; ++k) rc = rc || ((t[k] & 1) && ((t[k] >> 5) & 3) == kLpMfmaRc);
+        if (rc && d.thr[s] / 64 < nnt) {
+            why = "launch " + std::to_string(s) + " has " + std::to_string(d.thr[s] / 64) + " waves for " +
+                  std::to_string(nnt) + " MFMA low-pass column tiles";
+            return false;
+        }
+    }
+    return true;
 }
 
 int copy_words(const std::vector<int>& w, int32_t* out, int64_t max_words, int64_t* nwords) {
@@ -1827,6 +1855,11 @@ int wst_describe_variants(int M, int N, int J, int L, int max_order, int32_t* ou
     wst_plan* p = nullptr;
     const int rc = create_plan(M, N, J, L, max_order, 0, nullptr, false, &p);
     if (rc != WST_OK) return rc;
+    std::string why;   // the device plan's launch-shape check, here too (the CPU sweep runs it)
+    if (!rc_waves_ok(p, why)) {
+        free_plan(p);
+        return fail(WST_ERR_INVALID, why);
+    }
     const std::vector<int> w = describe_chunk(p);
     free_plan(p);
     return copy_words(w, out, max_words, nwords);
