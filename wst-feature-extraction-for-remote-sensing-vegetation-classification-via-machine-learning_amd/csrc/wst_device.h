@@ -774,13 +774,13 @@ __device__ __forceinline__ void lds_lowpass_mfma_rc(float2* U, int nb, int bs, i
     }
     // 1. T = U GN: every wave keeps one column tile (waves w and w + nnt share it, splitting its
     //    row tiles).  Needs nw >= nnt: the plan checks it for every launch that takes this form
-    //    (wst_hip.hip, rc_waves_ok); the max() only keeps a violating launch from spinning.  (A
+    //    (wst_hip.hip, rc_waves_ok).  (A
     //    nested loop serving nw < nnt here cost the f3 k_o2 1.8 %, measured round 5.)
     {
         float g[KS];
         const int nt = wave % nnt;
         load_ops(GN, nnt, nt, g);
-        for (int tk = wave / nnt; tk < nb * NMT; tk += max(1, nw / nnt)) {
+        for (int tk = wave / nnt; tk < nb * NMT; tk += nw / nnt) {
             const int b = tk / NMT, mt = tk - b * NMT;
             float2* Ub = U + b * bs;
             const int p = mt * 16 + li;
@@ -1790,10 +1790,12 @@ __device__ __forceinline__ void prep_body(unsigned char* smem, const DevParams& 
     lds_fft2<FM, FN, 0, wstfft::kMaxFamilyN, kNat, false>(A, 1, 0, PM, PN, ld, tb.twM(0), tb.twN(0), id);
     float2* dst = xhat + local * n;
     for (GridIter it(PN); it.u < PM; it.next()) dst[it.u * PN + it.v] = A[it.u * ld + it.v];
+#ifdef WST_TRACE
     if (tracing(p, get_tslot(lay))) {   // (after the work: the body is laid out as without it)
         trace_word(p, get_tslot(lay), 0, tr_kernel(kTkPrep, FM, FN, 0, 0, 0));
         trace_word(p, get_tslot(lay), 1, tr_prep(PC, wide_lowpass(p) ? (mfma_rc_ok<PC>() ? kLpMfmaRc : kLpMfma) : kLpPlain));
     }
+#endif
 }
 
 // One workgroup per plane.  Square planes of the family's sizes in (48, 136] run with compile-time
@@ -1984,6 +1986,12 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
 // it): the same compile-time constants and run-time tests the body's dispatch used.
 template <int FM, int FN, int MAXN, int SQ, int OC, int N1T = 0>
 __device__ __forceinline__ void trace_o1(const DevParams& p, const LdsLayout& lay, int j1) {
+#ifndef WST_TRACE
+    (void)p;
+    (void)lay;
+    (void)j1;
+    return;
+#endif
     if (!tracing(p, get_tslot(lay))) return;
     constexpr int N1C = N1T ? N1T : SQ ? unique_level(FM, MAXN) : 0;
     constexpr bool FUSE1 = SQ && N1C >= kFuse1Min && wstfft::LineFFT<(N1C > 0 ? N1C : 2), true>::N2 > 1;
@@ -2221,96 +2229,104 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             // that batch's transform barriers (emit above reads S alone)
         }
     };
-    // The order-2 levels of this launch and their compile-time shapes, in one place: `fn` is
-    // called once per level as fn(branch, j2, nM2, nN2, PB, SC, NC).  The trace pass (below) and
-    // the work run the same dispatch, so the trace records the path the work takes.
-    auto dispatch = [&](auto&& fn, int& br) __attribute__((always_inline)) {
-        br = 7;
-        if constexpr (N1C > 0) {
-            br = 1;
-            // compile-time level sizes N1C / 2^k (the paths of an SQ launch start at j2 = j1 + 1)
-            wstfft::static_for<1, 8>([&](auto kc) {
-                constexpr int k = decltype(kc)::value;
-                constexpr int NN2 = N1C >> k;
-                if constexpr ((NN2 << k) == N1C && NN2 >= 1)
-                    if (j1 + k < J && j1 + k >= j2first)
-                        fn(j1 + k, NN2, NN2,
-                              std::integral_constant<int, LC == 0 ? 0 : (k == 1 && MAXN > kWholeFirstCap) ? 2 : LC>{},
-                              std::integral_constant<int, (1 << k)>{}, std::integral_constant<int, NN2>{});
-            });
-        } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {
-            // after a big level the paths start at the first LDS-resident level, which is the
-            // family's single size of this class (> 136 / 2): compile-time sizes from there on
-            // (runtime sizes when a plan stages that level too and starts further down)
-            constexpr int N2C = unique_level(FM, MAXN);
-            if (j2first == j1 + 1 && (PM >> j1) == N2C && PM == PN) {
-                br = 2;
-                // exported spectrum of a resident level of the class's single size (k_o1 finished
-                // the column FFTs): compile-time path sizes N2C / 2^k and tile-mapped folds from HBM
-                wstfft::static_for<1, 8>([&](auto kc) {
-                    constexpr int k = decltype(kc)::value;
-                    constexpr int NN2 = N2C >> k;
-                    if constexpr ((NN2 << k) == N2C && NN2 >= 1)
-                        if (j1 + k < J)
-                            fn(j1 + k, NN2, NN2, std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
-                                  std::integral_constant<int, (1 << k)>{}, std::integral_constant<int, NN2>{});
-                });
-            } else if ((PM >> j2first) == N2C) {
-                br = 3;
-                wstfft::static_for<0, 8>([&](auto kc) {
-                    constexpr int k = decltype(kc)::value;
-                    constexpr int NN2 = N2C >> k;
-                    if constexpr ((NN2 << k) == N2C && NN2 >= 1)
-                        if (j2first + k < J) fn(j2first + k, NN2, NN2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
-                      std::integral_constant<int, 0>{});
-                });
-            } else {
-                br = 4;
-                for (int j2 = j2first; j2 < J; ++j2) fn(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
-                      std::integral_constant<int, 0>{});
-            }
-        } else if constexpr (!SQ && HG == 1 && FM == FN && FM > 0) {
-            // exported-spectrum k_o2 (f3 / c1): a square level of one of the family's sizes in this
-            // class runs with compile-time path sizes (and, with LC, compile-time batch shapes)
-            bool done = false;
-            br = 6;
-            if (PM == PN && j2first == j1 + 1) {
-                wstfft::static_for<0, 8>([&](auto mc) {
-                    constexpr int N1X = FM << decltype(mc)::value;
-                    if constexpr (N1X <= MAXN && N1X > prev_cap(MAXN)) {
-                        if (!done && (PM >> j1) == N1X) {
-                            done = true;
-                            br = 5;
-                            wstfft::static_for<1, 8>([&](auto kc) {
-                                constexpr int k = decltype(kc)::value;
-                                constexpr int NN2 = N1X >> k;
-                                if constexpr ((NN2 << k) == N1X && NN2 >= 1)
-                                    if (j1 + k < J)
-                                        fn(j1 + k, NN2, NN2,
-                                              std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},
-                                              std::integral_constant<int, 0>{}, std::integral_constant<int, NN2>{});
-                            });
-                        }
-                    }
-                });
-            }
-            if (!done)
-                for (int j2 = j2first; j2 < J; ++j2) fn(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
-                      std::integral_constant<int, 0>{});
-        } else {
-            for (int j2 = j2first; j2 < J; ++j2) fn(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},
-                      std::integral_constant<int, 0>{});
-        }
-    };
-    int br_run = 0;
-    dispatch(level, br_run);
+    // The order-2 levels of this launch and their compile-time shapes, in one place: FN_ is
+    // called once per level as FN_(j2, nM2, nN2, PB, SC, NC).  The trace pass (below) and the
+    // work expand the same dispatch, so the trace records the path the work takes.  (A macro,
+    // not a lambda taking the functor: the lambda form cost the f3 k_o2 1 % -- 1570 more
+    // instructions, SGPR spills from the kernel entry on; measured round 5.)
+    // Branches: N1C > 0 -- compile-time level sizes N1C / 2^k (an SQ launch's paths start at
+    // j2 = j1 + 1); SQ HG -- after a big level the paths start at the first LDS-resident level,
+    // the family's single size of this class (> 136 / 2): compile-time sizes from there on (from
+    // the exported spectrum with tile-mapped folds when k_o1 finished that level's column FFTs;
+    // runtime sizes when a plan stages that level too and starts further down); !SQ HG (f3 / c1)
+    // -- a square level of one of the family's sizes runs with compile-time path sizes (and, with
+    // LC, compile-time batch shapes); otherwise runtime sizes.
+#define WST_O2_DISPATCH(FN_)                                                                                                                      \
+    if constexpr (N1C > 0) {                                                                                                                      \
+        wstfft::static_for<1, 8>([&](auto kc) {                                                                                                   \
+            constexpr int k = decltype(kc)::value;                                                                                                \
+            constexpr int NN2 = N1C >> k;                                                                                                         \
+            if constexpr ((NN2 << k) == N1C && NN2 >= 1)                                                                                          \
+                if (j1 + k < J && j1 + k >= j2first)                                                                                              \
+                    FN_(j1 + k, NN2, NN2,                                                                                                         \
+                          std::integral_constant<int, LC == 0 ? 0 : (k == 1 && MAXN > kWholeFirstCap) ? 2 : LC>{},                                \
+                          std::integral_constant<int, (1 << k)>{}, std::integral_constant<int, NN2>{});                                           \
+        });                                                                                                                                       \
+    } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {                                                                           \
+        constexpr int N2C = unique_level(FM, MAXN);                                                                                               \
+        if (j2first == j1 + 1 && (PM >> j1) == N2C && PM == PN) {                                                                                 \
+            wstfft::static_for<1, 8>([&](auto kc) {                                                                                               \
+                constexpr int k = decltype(kc)::value;                                                                                            \
+                constexpr int NN2 = N2C >> k;                                                                                                     \
+                if constexpr ((NN2 << k) == N2C && NN2 >= 1)                                                                                      \
+                    if (j1 + k < J)                                                                                                               \
+                        FN_(j1 + k, NN2, NN2, std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},                                       \
+                              std::integral_constant<int, (1 << k)>{}, std::integral_constant<int, NN2>{});                                       \
+            });                                                                                                                                   \
+        } else if ((PM >> j2first) == N2C) {                                                                                                      \
+            wstfft::static_for<0, 8>([&](auto kc) {                                                                                               \
+                constexpr int k = decltype(kc)::value;                                                                                            \
+                constexpr int NN2 = N2C >> k;                                                                                                     \
+                if constexpr ((NN2 << k) == N2C && NN2 >= 1)                                                                                      \
+                    if (j2first + k < J) FN_(j2first + k, NN2, NN2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},           \
+                  std::integral_constant<int, 0>{});                                                                                              \
+            });                                                                                                                                   \
+        } else {                                                                                                                                  \
+            for (int j2 = j2first; j2 < J; ++j2) FN_(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},  \
+                  std::integral_constant<int, 0>{});                                                                                              \
+        }                                                                                                                                         \
+    } else if constexpr (!SQ && HG == 1 && FM == FN && FM > 0) {                                                                                  \
+        bool done = false;                                                                                                                        \
+        if (PM == PN && j2first == j1 + 1) {                                                                                                      \
+            wstfft::static_for<0, 8>([&](auto mc) {                                                                                               \
+                constexpr int N1X = FM << decltype(mc)::value;                                                                                    \
+                if constexpr (N1X <= MAXN && N1X > prev_cap(MAXN)) {                                                                              \
+                    if (!done && (PM >> j1) == N1X) {                                                                                             \
+                        done = true;                                                                                                              \
+                        wstfft::static_for<1, 8>([&](auto kc) {                                                                                   \
+                            constexpr int k = decltype(kc)::value;                                                                                \
+                            constexpr int NN2 = N1X >> k;                                                                                         \
+                            if constexpr ((NN2 << k) == N1X && NN2 >= 1)                                                                          \
+                                if (j1 + k < J)                                                                                                   \
+                                    FN_(j1 + k, NN2, NN2,                                                                                         \
+                                          std::integral_constant<int, LC == 0 ? 0 : k == 1 ? 2 : LC>{},                                           \
+                                          std::integral_constant<int, 0>{}, std::integral_constant<int, NN2>{});                                  \
+                        });                                                                                                                       \
+                    }                                                                                                                             \
+                }                                                                                                                                 \
+            });                                                                                                                                   \
+        }                                                                                                                                         \
+        if (!done)                                                                                                                                \
+            for (int j2 = j2first; j2 < J; ++j2) FN_(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},  \
+                  std::integral_constant<int, 0>{});                                                                                              \
+    } else {                                                                                                                                      \
+        for (int j2 = j2first; j2 < J; ++j2) FN_(j2, PM >> j2, PN >> j2, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{},      \
+                  std::integral_constant<int, 0>{});                                                                                              \
+    }
+    WST_O2_DISPATCH(level)
+#ifdef WST_TRACE   // (the trace build only: not even dead code in the product)
     if (tracing(p, get_tslot(lay))) {
         // trace pass, after the work (the hot code's layout and registers stay as without it):
         // the same dispatch with a functor that only records each level's path
         constexpr int spec = HG ? 0 : (N1C > 0 && wstfft::LineFFT<(N1C > 0 ? N1C : 2), false>::N2 > 1) ? 1 : 2;
-        int br = 0;
+        // the branch the dispatch takes (same tests, in the same order)
+        int br = 7;
+        if constexpr (N1C > 0) {
+            br = 1;
+        } else if constexpr (SQ && HG == 1 && unique_level(FM, MAXN) > 0) {
+            constexpr int N2C = unique_level(FM, MAXN);
+            br = (j2first == j1 + 1 && (PM >> j1) == N2C && PM == PN) ? 2 : (PM >> j2first) == N2C ? 3 : 4;
+        } else if constexpr (!SQ && HG == 1 && FM == FN && FM > 0) {
+            br = 6;
+            if (PM == PN && j2first == j1 + 1)
+                wstfft::static_for<0, 8>([&](auto mc) {
+                    constexpr int N1X = FM << decltype(mc)::value;
+                    if constexpr (N1X <= MAXN && N1X > prev_cap(MAXN))
+                        if ((PM >> j1) == N1X) br = 5;
+                });
+        }
         const int lpw = wide_lowpass(p) ? 1 : 0;
-        dispatch([&](int j2, int, int, auto pbc, auto scc, auto ncc) __attribute__((always_inline)) {
+        auto record = [&](int j2, int, int, auto pbc, auto scc, auto ncc) __attribute__((always_inline)) {
             constexpr int PB = decltype(pbc)::value, SC = decltype(scc)::value, NC = decltype(ncc)::value;
             constexpr int N1F = (SQ && NC > 0 && SC > 0) ? NC * SC : 0;
             constexpr bool FUSE = N1F > 0 && SC == 2 && N1F / 2 >= kFuseMin &&
@@ -2322,10 +2338,13 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             if (2 + (j2 - j1 - 1) < kTraceW)
                 trace_word(p, get_tslot(lay), 2 + (j2 - j1 - 1),
                            tr_level(j2, PB, SC, NC, fk ? fk : (s2 == 2 ? kFdDenseS2 : kFdBox), lpk, s2));
-        }, br);
+        };
+        WST_O2_DISPATCH(record)
         trace_word(p, get_tslot(lay), 0, tr_kernel(kTkO2, FM, FN, MAXN, SQ, HG));
         trace_word(p, get_tslot(lay), 1, tr_o2(OC, LC, N1C, spec, br));
     }
+#endif
+#undef WST_O2_DISPATCH
 }
 
 
