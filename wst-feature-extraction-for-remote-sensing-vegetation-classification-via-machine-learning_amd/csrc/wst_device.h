@@ -940,6 +940,12 @@ __device__ __forceinline__ void lds_lowpass_taps(float2* U, int rows, int cols, 
 // RS > 0: the rows were transformed with the split N = (NN / RS) x RS (fused_row_n2), so physical
 // column q holds another logical column than GN's rows (split_n2 order) assume: the S pass walks
 // GN's order and reads each column's partial from its position in the rows' order.
+// Address-space-typed pointers (global / LDS) for stores the compiler must not merge into flat ones
+typedef __attribute__((address_space(1))) float* gfloat_p;
+typedef __attribute__((address_space(3))) float* lfloat_p;
+typedef const __attribute__((address_space(1))) float* gcfloat_p;
+typedef const __attribute__((address_space(3))) float* lcfloat_p;
+
 template <int NN, int RS = 0>
 __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, int ld,
                                            const float2* tw, const float* GM, const float* GN,
@@ -1056,8 +1062,10 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
         }
         acc = group_sum<QC>(acc);
         if (qc == 0) {
-            if (outd) __builtin_nontemporal_store(acc, outd + o);
-            else S[o] = acc;
+            // typed global / LDS pointers: as one generic pointer the compiler merges the two stores
+            // into a flat store, which the next LDS wait (and barrier) must see complete in HBM
+            if (outd) __builtin_nontemporal_store(acc, (gfloat_p)outd + o);
+            else ((lfloat_p)S)[o] = acc;
         }
     }
     __syncthreads();

@@ -438,74 +438,78 @@ __global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a
     float* csum_t = reinterpret_cast<float*>(A + C * ld) + (a.g_lds ? n * a.oms : 0);
     wstdev::EpiModulus mod{a.scale, 0.f};
     big_fft<N, INV>(A, wstfft::Lines(1, 0, nc, ld, 1), n, tw, mod);
-    // V[q][a] = sum_p GMnat[p][a] m[p][q] (a < oM) and the column sum: the taps are staged in LDS
-    // after the column tile (when they fit), one thread per (column, 16-row chunk) accumulates
-    // every output of its rows, then the 16 chunks of a column are shuffle-reduced
     const int oms = a.oms;
-    const float* G = a.gnat;
-    if (a.g_lds) {
-        float* Gl = reinterpret_cast<float*>(A + C * ld);   // n x oms taps after the column tile
+    float* Gl = reinterpret_cast<float*>(A + C * ld);   // n x oms taps after the column tile
+    if (a.g_lds)
         for (int i = threadIdx.x; i < n * oms; i += T) Gl[i] = a.gnat[i];
-        G = Gl;
-    }
     __syncthreads();
-    constexpr int PC = 16;
-    if (p.oM <= 8) {
-        for (int w = threadIdx.x; w < nc * PC; w += T) {
-            const int pc = w & (PC - 1);
-            const int c = w / PC;
-            const float2* col = A + c * ld;
-            float acc[9];
+    // the tap reads typed by where the taps are (LDS / global): through one generic pointer they
+    // are flat loads, and every wait on them waits for both the LDS and the memory counter
+    auto partials = [&](auto G) __attribute__((always_inline)) {
+        constexpr int PC = 16;
+        if (p.oM <= 8) {
+            for (int w = threadIdx.x; w < nc * PC; w += T) {
+                const int pc = w & (PC - 1);
+                const int c = w / PC;
+                const float2* col = A + c * ld;
+                float acc[9];
 #pragma unroll
-            for (int k = 0; k < 9; ++k) acc[k] = 0.f;
-            for (int u = pc; u < n; u += PC) {
-                const float mv = col[u].x;
-                const float* g = G + u * oms;
+                for (int k = 0; k < 9; ++k) acc[k] = 0.f;
+                for (int u = pc; u < n; u += PC) {
+                    const float mv = col[u].x;
+                    const auto g = G + u * oms;
 #pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    if (k < p.oM) acc[k] = fmaf(g[k], mv, acc[k]);
-                acc[8] += mv;
+                    for (int k = 0; k < 8; ++k)
+                        if (k < p.oM) acc[k] = fmaf(g[k], mv, acc[k]);
+                    acc[8] += mv;
+                }
+#pragma unroll
+                for (int k = 0; k < 9; ++k) acc[k] = wstdev::group_sum<PC>(acc[k]);
+                if (pc == 0) {
+                    for (int k = 0; k < p.oM; ++k) a.vpart[(static_cast<long long>(arr) * a.ncols + c0 + c) * oms + k] = acc[k];
+                    a.csum[static_cast<long long>(arr) * a.ncols + c0 + c] = acc[8];
+                    csum_t[c] = acc[8];
+                }
             }
-#pragma unroll
-            for (int k = 0; k < 9; ++k) acc[k] = wstdev::group_sum<PC>(acc[k]);
-            if (pc == 0) {
-                for (int k = 0; k < p.oM; ++k) a.vpart[(static_cast<long long>(arr) * a.ncols + c0 + c) * oms + k] = acc[k];
-                a.csum[static_cast<long long>(arr) * a.ncols + c0 + c] = acc[8];
-                csum_t[c] = acc[8];
-            }
+            return;
         }
-        if (a.mode == kColModLpFwd) col_spectra<N>(A, tw, a, arr, c0, nc, n, csum_t);
-        return;
-    }
-    // wide output maps: kBigOGroup outputs per round over the column tile held in LDS
-    for (int a0 = 0; a0 < p.oM; a0 += kBigOGroup) {
-        for (int w = threadIdx.x; w < nc * PC; w += T) {
-            const int pc = w & (PC - 1);
-            const int c = w / PC;
-            const float2* col = A + c * ld;
-            float acc[kBigOGroup + 1];
+        // wide output maps: kBigOGroup outputs per round over the column tile held in LDS
+        for (int a0 = 0; a0 < p.oM; a0 += kBigOGroup) {
+            for (int w = threadIdx.x; w < nc * PC; w += T) {
+                const int pc = w & (PC - 1);
+                const int c = w / PC;
+                const float2* col = A + c * ld;
+                float acc[kBigOGroup + 1];
 #pragma unroll
-            for (int k = 0; k <= kBigOGroup; ++k) acc[k] = 0.f;
-            for (int u = pc; u < n; u += PC) {
-                const float mv = col[u].x;
-                const float* g = G + u * oms + a0;
+                for (int k = 0; k <= kBigOGroup; ++k) acc[k] = 0.f;
+                for (int u = pc; u < n; u += PC) {
+                    const float mv = col[u].x;
+                    const auto g = G + u * oms + a0;
 #pragma unroll
-                for (int k = 0; k < kBigOGroup; ++k)
-                    if (a0 + k < p.oM) acc[k] = fmaf(g[k], mv, acc[k]);
-                acc[kBigOGroup] += mv;
-            }
+                    for (int k = 0; k < kBigOGroup; ++k)
+                        if (a0 + k < p.oM) acc[k] = fmaf(g[k], mv, acc[k]);
+                    acc[kBigOGroup] += mv;
+                }
 #pragma unroll
-            for (int k = 0; k <= kBigOGroup; ++k) acc[k] = wstdev::group_sum<PC>(acc[k]);
-            if (pc == 0) {
-                for (int k = 0; k < kBigOGroup && a0 + k < p.oM; ++k)
-                    a.vpart[(static_cast<long long>(arr) * a.ncols + c0 + c) * oms + a0 + k] = acc[k];
-                if (a0 == 0) {
-                    a.csum[static_cast<long long>(arr) * a.ncols + c0 + c] = acc[kBigOGroup];
-                    csum_t[c] = acc[kBigOGroup];
+                for (int k = 0; k <= kBigOGroup; ++k) acc[k] = wstdev::group_sum<PC>(acc[k]);
+                if (pc == 0) {
+                    for (int k = 0; k < kBigOGroup && a0 + k < p.oM; ++k)
+                        a.vpart[(static_cast<long long>(arr) * a.ncols + c0 + c) * oms + a0 + k] = acc[k];
+                    if (a0 == 0) {
+                        a.csum[static_cast<long long>(arr) * a.ncols + c0 + c] = acc[kBigOGroup];
+                        csum_t[c] = acc[kBigOGroup];
+                    }
                 }
             }
         }
-    }
+    };
+    // V[q][a] = sum_p GMnat[p][a] m[p][q] (a < oM) and the column sum: the taps are staged in LDS
+    // after the column tile (when they fit), one thread per (column, 16-row chunk) accumulates
+    // every output of its rows, then the 16 chunks of a column are shuffle-reduced
+    if (a.g_lds)
+        partials((wstdev::lcfloat_p)Gl);
+    else
+        partials((wstdev::gcfloat_p)a.gnat);
     if (a.mode == kColModLpFwd) col_spectra<N>(A, tw, a, arr, c0, nc, n, csum_t);
 }
 
