@@ -1045,8 +1045,7 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
         const int a = dc.div(ac);
         const int c = ac - a * oN;
         const float* f = reinterpret_cast<const float*>(U + b * bs + (a >> 1) * ld) + (a & 1);
-        float acc = 0.f;
-        for (int q = qc; q < cols; q += QC) {
+        auto column = [&](int q, float acc) __attribute__((always_inline)) {
             int qr = q;   // position of GN row q's logical column in the rows' order
             if constexpr (RS > 0) {
                 constexpr int N2d = wstfft::split_n2(NN), N1d = NN / N2d, N1r = NN / RS;
@@ -1058,8 +1057,16 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
                 constexpr int k = decltype(kc)::value;
                 wq += f[2 * (qr + RU * k * ld)];
             });
-            acc = fmaf(GN[q * oms + c], wq, acc);
-        }
+            return fmaf(GN[q * oms + c], wq, acc);
+        };
+        // the NN / QC columns of a lane unrolled (their LDS reads issue together: a rolled loop
+        // waited out the LDS latency once per column); same order of accumulation
+        constexpr int CQ = (NN + QC - 1) / QC;
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < CQ; ++i)
+            if (qc + i * QC < cols) acc = column(qc + i * QC, acc);
+        for (int q = qc + CQ * QC; q < cols; q += QC) acc = column(q, acc);
         acc = group_sum<QC>(acc);
         if (qc == 0) {
             // typed global / LDS pointers: as one generic pointer the compiler merges the two stores
