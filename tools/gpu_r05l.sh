@@ -1,0 +1,7 @@
+#!/bin/bash
+# Round-5 A/B: direct S2 contraction in the column pass's unit lanes vs the previous library (var_base)
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 99
+tools/gpu_step.sh 600 gpurun_out/r05l_pytest.txt python3 -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread || exit 99
+tail -2 gpurun_out/r05l_pytest.txt
+bash tools/ab_rep.sh r05l 3072,64,4 3 libwst_hip.so var_base.so || exit 99
+bash tools/ab_rep.sh r05l5 256,256,6,12 1 libwst_hip.so var_base.so || exit 99
