@@ -346,9 +346,12 @@ int rows_per_unit(int n) {
     return n2 == 1 ? n : n2;
 }
 
-// Bins of an order-2 filter pair below this fraction of the filter's maximum are skipped by the
-// box-sparse fold (dropped contribution < 1e-10 relative; measured 5e-11 in float64 at c2).
-constexpr double kBoxThreshold = 1e-10;
+// Bins of a filter (pair) below this fraction of the filter's maximum are skipped by the box-sparse
+// folds.  Zeroing every psi bin below it moves the float64 oracle's coefficients by at most
+// 1.7e-8 (64^2 J=4), 5.3e-9 (128^2 J=2), 2.5e-8 (256^2 J=6 L=12) of each coefficient's maximum --
+// below fp32 resolution (6e-8) and 400x below the 1e-5 parity bar (tools/box_threshold.py;
+// 1e-10, the round-1..4 value, kept 11 % more bins at c5).
+constexpr double kBoxThreshold = 1e-8;
 
 // Minimal cyclic window [i0, i0 + n) of Z_s covering the set bits of `hit` -> i0 | n << 8.
 int cyclic_window(const std::vector<char>& hit) {
