@@ -1399,9 +1399,9 @@ __device__ __forceinline__ float2 buf_load2(__amdgpu_buffer_rsrc_t r, int voff, 
 // Box-sparse: only the aliases i in [i0, i0 + ni) (mod s) of row u and j in [j0, j0 + nj) of
 // column v are summed, where the pair's alias boxes (host: box_bins) cover every bin at which
 // either filter exceeds kBoxThreshold * its maximum; the dropped terms are below that bound.
-// Column taps go in blocks of four, set up once per block (H column, mirror, sign and a zero
-// weight past the box -- the out-of-box alias stays a valid address), then the block walks the
-// box rows: per tap one LDS read, one buffer load (32-bit offsets) and the products.
+// Column taps go in blocks of four, set up once per block (H column, mirror, sign; taps past the
+// box are skipped), then the block walks the box rows: per tap one read of H, one buffer load
+// (32-bit offsets) and the products.
 template <int S>
 __device__ __forceinline__ void fold2(const float2* __restrict__ H, int hld, int nM1, int nN1,
                                       const float2* __restrict__ psi2, long long pstride,
@@ -1426,17 +1426,16 @@ __device__ __forceinline__ void fold2(const float2* __restrict__ H, int hld, int
         float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
         for (int jb = 0; jb < nj; jb += 4) {
             int hc[4], fc[4];
-            bool mir[4];
-            float wx[4], wy[4];
+            bool mir[4], ok[4];
+            float wy[4];
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                const bool ok = jb + c < nj;
+                ok[c] = jb + c < nj;
                 const int kc = v + ((j0 + jb + c) & smask) * nN2;
                 mir[c] = kc > half;
                 hc[c] = mir[c] ? nN1 - kc : kc;
                 fc[c] = kc * 8;
-                wx[c] = ok ? 1.f : 0.f;
-                wy[c] = ok ? (mir[c] ? -1.f : 1.f) : 0.f;
+                wy[c] = mir[c] ? -1.f : 1.f;
             }
             for (int i = 0; i < ni; ++i) {
                 const int kr = u + ((i0 + i) & smask) * nM2;
@@ -1445,14 +1444,20 @@ __device__ __forceinline__ void fold2(const float2* __restrict__ H, int hld, int
                 const float2* hm = H + krm * hld;
                 const int fo = (fpr + kr * nN1) * 8;
                 float2 hv[4], fv[4];
+                // taps past the box are not loaded (boxes are 1-3 aliases wide at c5's s >= 4
+                // levels: the padded block of 4 had loaded half its taps for nothing)
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    hv[c] = (mir[c] ? hm : hd)[hc[c]];
-                    fv[c] = buf_load2(rs, fo + fc[c], 0);
+                    hv[c] = make_float2(0.f, 0.f);
+                    fv[c] = make_float2(0.f, 0.f);
+                    if (ok[c]) {
+                        hv[c] = (mir[c] ? hm : hd)[hc[c]];
+                        fv[c] = buf_load2(rs, fo + fc[c], 0);
+                    }
                 }
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const float hx = hv[c].x * wx[c], hy = hv[c].y * wy[c];
+                    const float hx = hv[c].x, hy = hv[c].y * wy[c];
                     a0 = make_float2(fmaf(hx, fv[c].x, a0.x), fmaf(hy, fv[c].x, a0.y));
                     a1 = make_float2(fmaf(hx, fv[c].y, a1.x), fmaf(hy, fv[c].y, a1.y));
                 }
