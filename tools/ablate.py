@@ -17,11 +17,13 @@ sys.path.insert(0, os.getcwd())
 import numpy as np, torch, wst_amd
 from wst_amd import _lib
 _lib.use_library(os.environ["ABL_LIB"])
-B, M, J = (int(v) for v in os.environ.get("WST_KM_GEOM", "3072,64,4").split(","))
+geo = [int(v) for v in os.environ.get("WST_KM_GEOM", "3072,64,4").split(",")]
+B, M, J = geo[:3]
+L = geo[3] if len(geo) > 3 else 8
 x = torch.from_numpy(np.random.default_rng(1).integers(0,256,(B,M,M),dtype=np.uint8).astype(np.float32)/255).cuda()
-plan = _lib.Plan(M,M,J,8)
+plan = _lib.Plan(M,M,J,L)
 out = torch.empty((B, plan.K, plan.Mo, plan.No), device="cuda")
-wsb = plan.workspace_bytes(2048); ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+wsb = plan.workspace_bytes(min(B, plan.preferred_batch())); ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 for _ in range(2): plan.forward(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st)
 acc = [0.0]*(1+2*J)

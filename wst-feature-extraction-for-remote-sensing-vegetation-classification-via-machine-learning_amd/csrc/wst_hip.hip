@@ -331,7 +331,7 @@ size_t layout(LdsLayout& lay, size_t data_a, size_t data_b, const TableOffsets& 
 constexpr size_t kMaxStreamWs = 4;   // streams that keep an internal workspace per plan
 
 // paths per order-2 batch at level j2 (mirrors k_o2)
-constexpr int kHgSplit = 4;   // k_o2 HG workgroups per (plane, theta1)
+constexpr int kHgSplit = 1;   // k_o2 HG workgroups per (plane, theta1) (4 until round 5)
 constexpr int kHgGroup = 16;  // k_o2 HG items per batch-major dispatch group of an XCD
 
 int paths_per_batch(size_t bcap, size_t pslot, int L) {
@@ -982,7 +982,10 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
         // 10 workgroups per item, c5 29.66 / 29.08 / 29.35 / 30.09 ms).  Dispatch slots run
         // batch-major over groups of kHgGroup items, so the workgroups an XCD runs together fold the
         // same filter pairs (c5 split x group, ms/step: 3 x 1 26.29, 5 x 16 26.10, 4 x 16 25.89,
-        // 6 x 8 26.16; HG fetch per chunk at j1 = 0 / 1: 4.04 / 0.54 GB -> 2.46 / 0.27 GB at 4 x 16)
+        // 6 x 8 26.16; HG fetch per chunk at j1 = 0 / 1: 4.04 / 0.54 GB -> 2.46 / 0.27 GB at 4 x 16).
+        // Round 5: with the box fold loading only in-box taps the split no longer pays (c5 split
+        // 4 / 3 / 2 / 1: 23.49 / 23.39 / 23.11 / 23.06 ms per step, profiles/r05_ab.txt r05r): one
+        // workgroup per item; the split stays a diagnostic knob (WST_HG_SPLIT / WST_HG_GROUP)
         int nbatch = 0;
         for (int j2 = j2f; j2 < J; ++j2) {
             const int pb = paths_per_batch(bcap, pslot(j2), L);
