@@ -1409,7 +1409,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         plan->big_r[0]->rows(false, Launch{dim3(PM / a.rows, nimg), tb, plan->big_rows_lds[0], stream}, dp, a);
         BigArgs c = cargs(kColStore, 0, PN);
         c.dst = xhat;
-        plan->big_c[0]->cols(false, Launch{col_grid(PN, nimg), tb, plan->big_cols_lds[0], stream}, dp, c);
+        plan->big_c[0]->cols(false, Launch{col_grid(PN, nimg), dim3(wstbig::big_col_threads(plan->big_c[0]->n)), plan->big_cols_lds[0], stream}, dp, c);
         cm.final_(Launch{dim3(nimg), dim3(64), sbytes, stream}, dp, kFinalRows, 0, PM, PN, noms, part,
                   gnat(0, 0), nullptr, nullptr, L, 0, 0, 0, 1, img0, d_out, pooled);
     }
@@ -1435,7 +1435,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
         c.csum = csum;
         c.scale = 1.f / (static_cast<float>(g.PM) * static_cast<float>(g.PN));
         c.gnat = gnat(j1, 0);
-        plan->big_c[j1]->cols(true, Launch{col_grid(n1, nimg * L), tb, plan->big_cols_lds[j1], stream}, dp, c);
+        plan->big_c[j1]->cols(true, Launch{col_grid(n1, nimg * L), dim3(wstbig::big_col_threads(plan->big_c[j1]->n)), plan->big_cols_lds[j1], stream}, dp, c);
         cm.final_(Launch{dim3(nimg * L), dim3(64), sbytes, stream}, dp, kFinalCols, 1, n1, m1, noms, part,
                   gnat(j1, 1), csum, do2 ? umean : nullptr, L, j1, 0, 0, 1, img0, d_out, pooled);
         if (do2) {
@@ -1483,7 +1483,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
                 mc.csum = csum + static_cast<size_t>(l1) * nimg * L * n2;
                 mc.scale = 1.f / (static_cast<float>(m1) * static_cast<float>(n1));
                 mc.gnat = gnat(j2, 0);
-                plan->big_c[j2]->cols(true, Launch{col_grid(n2, nimg * L), tb, plan->big_cols_lds[j2], stream}, dp, mc);
+                plan->big_c[j2]->cols(true, Launch{col_grid(n2, nimg * L), dim3(wstbig::big_col_threads(plan->big_c[j2]->n)), plan->big_cols_lds[j2], stream}, dp, mc);
             }
             // S2 of every theta1 in one launch (l1 = -1: blockIdx.y)
             cm.final_(Launch{dim3(nimg * L, L), dim3(64), sbytes, stream}, dp, kFinalCols, 2, n2, m2, noms,
@@ -1766,7 +1766,7 @@ void describe_o2(Describe& d, int j1, const LdsLayout& lay, int MAXN, int sq, in
 }
 
 void describe_big(Describe& d, bool rows, int n, bool inv, int body) {
-    int* t = d.site(wstbig::kBigThreads);
+    int* t = d.site(rows ? wstbig::kBigThreads : wstbig::big_col_threads(n));
     t[0] = tr_kernel(rows ? kTkBigRows : kTkBigCols, 0, 0, n, 0, inv ? 1 : 0);
     t[1] = body;
 }

@@ -30,7 +30,12 @@ namespace wstbig {
 using wstdev::DevParams;
 
 constexpr int kBigMinN = wstfft::kMaxFamilyN;   // levels with n > kBigMinN are staged
-constexpr int kBigThreads = 256;
+constexpr int kBigThreads = 256;   // row passes, plane means (512: c5 +5 %, measured round 5)
+// Column-pass workgroup by line length: the 384- and 512-point tiles (58-70 KB, two workgroups per
+// CU) keep more loads in flight with 512 threads (c5's 384^2 order-1 column pass 5.54 -> 5.10 ms
+// per step), the shorter ones hold more workgroups per CU and lose with it (192: +0.2 / +1.1 ms;
+// 1024 threads: worse everywhere).  0 = runtime length.
+constexpr int big_col_threads(int n) { return n >= 384 ? 512 : 256; }
 constexpr int kColTile = 16;         // columns per column-pass workgroup (128 B rows)
 constexpr int kMeanParts = 16;                  // k_big_mean partial sums per plane
 constexpr int kLoadBatch = 8;                   // global loads per thread in flight (tile loads)
@@ -384,7 +389,7 @@ __device__ __forceinline__ void col_spectra(float2* A, const float2* tw, const B
 // column pass: kColTile columns of one array per workgroup, each column contiguous in LDS
 // --------------------------------------------------------------------------------------------
 template <int N, bool INV>
-__global__ void __launch_bounds__(kBigThreads) k_big_cols(DevParams p, BigArgs a) {
+__global__ void __launch_bounds__(big_col_threads(N)) k_big_cols(DevParams p, BigArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int n = N > 0 ? N : a.n;
     const int ld = n | 1;
