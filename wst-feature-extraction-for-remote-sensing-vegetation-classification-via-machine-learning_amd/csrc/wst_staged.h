@@ -534,6 +534,7 @@ __global__ void __launch_bounds__(kBigThreads) k_big_mean(DevParams p, const flo
     float s = 0.f;
     for (int u = u0; u < u1; ++u) {
         const int su = p.pre_pad ? u : wstdev::reflect_index(u - p.padTop, p.M);
+#pragma unroll 4
         for (int v = threadIdx.x; v < PN; v += blockDim.x) {
             const int sv = p.pre_pad ? v : wstdev::reflect_index(v - p.padLeft, p.N);
             s += x[su * inN + sv];
@@ -575,10 +576,15 @@ __global__ void __launch_bounds__(64) k_big_final(DevParams p, int fmode, int ki
         const int o = w / KS, ks = w - o * KS;
         const int ra = o / p.oN, c = o - (o / p.oN) * p.oN;
         float acc = 0.f;
-        if (fmode == kFinalRows)
+        // unrolled so the loads of eight steps issue before the first use (a rolled loop waited out
+        // the memory latency once per step: ~27 us per launch at c5); same order of accumulation
+        if (fmode == kFinalRows) {
+#pragma unroll 8
             for (int k = ks; k < n; k += KS) acc = fmaf(G[k * oms + ra], P[k * oms + c], acc);
-        else
+        } else {
+#pragma unroll 8
             for (int k = ks; k < n; k += KS) acc = fmaf(G[k * oms + c], P[k * oms + ra], acc);
+        }
         if (KS == 4) acc = wstdev::group_sum<4>(acc);
         else if (KS == 2) acc = wstdev::group_sum<2>(acc);
         if (ks == 0) S[o] = acc;
