@@ -1417,7 +1417,7 @@ int staged_levels(const wst_plan* plan, const float* in, int nimg, long long img
     if ((rc = timer.end(stream, 0)) != WST_OK) return rc;
 
     for (int j1 = 0; j1 < plan->rb; ++j1) {
-        const int m1 = PM >> j1, n1 = PN >> j1, hld = n1 / 2 + 1;
+        const int m1 = PM >> j1, n1 = PN >> j1;
         const bool do2 = g.max_order >= 2 && j1 < J - 1;
         float2* hbig = do2 ? reinterpret_cast<float2*>(base + plan->ws_hbig[j1] * chunk) : nullptr;
         // ---- order 1: fold + inverse rows, inverse columns + |.| + low-pass partials, S1 ----
