@@ -157,8 +157,14 @@ int wst_forward_profiled(const wst_plan* plan, const float* d_in, int64_t nbatch
  *                           launches record the words they actually ran.  Only in the trace build
  *                           (libwst_hip_trace.so = the same sources with -DWST_TRACE); the product
  *                           library has no trace code and returns WST_ERR_UNSUPPORTED for enable.
+ *                           Needs a quiescent plan: call it with no forward of this plan in flight
+ *                           or being issued on another thread (it drains the device and takes the
+ *                           plan's workspace lock, but forwards with caller workspaces do not take
+ *                           that lock).  WST_ERR_UNSUPPORTED for plans with more launch sites per
+ *                           chunk than the trace area holds (512).
  *   wst_plan_read_trace   : copy the device trace (synchronises the device); *nwords = the
- *                           plan's site count x 12.
+ *                           plan's site count x 12 (never truncated: WST_ERR_UNSUPPORTED above 512
+ *                           sites).
  * out may be NULL for a size query in the first two (then only *nwords is set).
  */
 int wst_plan_variants(const wst_plan* plan, int32_t* out, int64_t max_words, int64_t* nwords);

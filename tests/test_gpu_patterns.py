@@ -16,57 +16,26 @@ Bars (tests/parity.py):
   gradients and 2-4e-4 on the edge, and even exceeds the per-coefficient 1e-5 bar on the gradients
   (1.7e-5), which the HIP path holds.
 
-The generators below are this repository's own restatement of those pattern definitions (input
-data only).  They exercise what random uint8 noise does not: constant rows / columns meeting the
-reflect padding (gradients), energy concentrated at the highest frequencies (checkerboard), a
-single bin (impulse) and large flat regions with sharp edges.
+The generators (tests/patterns.py) are this repository's own restatement of those pattern
+definitions (input data only).
+
+At BASELINE config 5's geometry (256^2, J=6, L=12) the box-sparse folds keep only 1-2 % of the alias
+taps (bins below kBoxThreshold = 1e-8 of a filter's maximum are skipped): the structured planes there
+come from a committed golden (tests/golden/make_pattern_golden.py) that
+also holds the fp32 pocketfft cascade's error on each plane, and run with the same bars.
 """
+import os
+
 import numpy as np
 import pytest
 
 from oracle import kymatio_ref as kr
-from parity import TOL, assert_parity, elementwise_error
+from parity import TOL, assert_parity, elementwise_error, per_coef_error
+from patterns import fp32_cascade, patterns
 
 from wst_amd.numpy import Scattering2D as NpS
 
 pytestmark = pytest.mark.gpu
-
-
-def patterns(n):
-    t = np.linspace(0.0, 1.0, n)
-    out = {
-        "gradient_h": np.tile(t, (n, 1)),
-        "gradient_v": np.tile(t[:, None], (1, n)),
-    }
-    sq = n // 8
-    ij = np.add.outer(np.arange(n) // sq, np.arange(n) // sq)
-    out["checkerboard"] = (ij % 2 == 0).astype(np.float64)
-    yy, xx = np.mgrid[0:n, 0:n]
-    r = np.hypot(yy - n / 2, xx - n / 2) / (n / 2)
-    out["circles"] = np.sin(r * 5 * np.pi) * 0.5 + 0.5
-    rng = np.random.RandomState(42)
-    out["texture"] = rng.rand(n, n)
-    stripes = (np.sin(np.linspace(0, 8 * 2 * np.pi, n))[None, :].repeat(n, 0) + 1) / 2
-    out["vertical_texture"] = np.clip(stripes * 0.7 + rng.rand(n, n) * 0.3, 0, 1)
-    edge = np.zeros((n, n))
-    b = n * 20 // 128
-    edge[b:n - b, b:n - b] = 1.0
-    out["edge"] = edge
-    imp = np.zeros((n, n))
-    imp[n // 3, n // 2] = 1.0
-    out["impulse"] = imp
-    return {k: v.astype(np.float32) for k, v in out.items()}
-
-
-def fp32_cascade(sc, x):
-    """The oracle's cascade (kymatio_ref.scattering2d) run with float32 input and filters, so every
-    FFT is scipy's single-precision pocketfft: the fp32 noise floor of the reference algorithm."""
-    def f32(d):
-        return {**d, "levels": [np.asarray(v, np.float32) for v in d["levels"]]}
-    out = kr.scattering2d(np.asarray(x, np.float32), lambda v: kr.reflect_pad(v, sc.pad_size),
-                          sc.J, sc.L, f32(sc.phi), [f32(p) for p in sc.psi], sc.max_order)
-    assert out.dtype == np.float32
-    return out
 
 
 @pytest.mark.parametrize("n,J", [(128, 2), (64, 4)])
@@ -87,4 +56,32 @@ def test_structured_patterns_against_oracle(n, J):
         assert_parity(g, r, what=what, floor=floor, elementwise=False)
         ew = elementwise_error(g, r, floor=floor).max()
         bar = max(TOL, 2.0 * elementwise_error(f32[i:i + 1], r, floor=floor).max())
+        assert ew <= bar, f"{what}: elementwise {ew:.3e} > bar {bar:.3e} (fp32 pocketfft x2 or 1e-5)"
+
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_structured_patterns_c5_geometry():
+    """BASELINE config 5 geometry (one band of 256^2, J=6, L=12: levels 384^2 / 192^2 HBM-staged,
+    folds at s = 16 / 32 keeping 1-2 % of the alias taps) on the gradients, checkerboard, edge and
+    impulse, with the bars of test_structured_patterns_against_oracle -- except that on the edge
+    the reference algorithm computed in fp32 (scipy pocketfft) itself misses the per-coefficient
+    1e-5 (1.7e-5, a coefficient whose map is mostly flat): there the bar is that fp32 error."""
+    d = np.load(os.path.join(GOLDEN, "c5_patterns_256_J6_L12.npz"))
+    x, ref = d["x"], d["S"].astype(np.float64)
+    got = NpS(J=int(d["J"]), shape=x.shape[-2:], L=int(d["L"]))(x)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    for i, name in enumerate(str(n) for n in d["names"]):
+        what = f"{name} 256x256 J=6 L=12"
+        floor = 1e-3 if name.startswith("gradient") else 0.0
+        g, r = got[i:i + 1], ref[i:i + 1]
+        # per coefficient: 1e-5, or where the reference algorithm in fp32 (pocketfft) misses 1e-5
+        # itself on this plane (the edge: 1.7e-5), no worse than it
+        pbar = max(TOL, float(d["f32_per_coef"][i].max()))
+        pc = per_coef_error(g, r, floor).max()
+        assert pc <= pbar, f"{what}: per-coefficient {pc:.3e} > bar {pbar:.3e} (1e-5 or fp32 pocketfft)"
+        ew = elementwise_error(g, r, floor=floor).max()
+        bar = max(TOL, 2.0 * float(d["f32_elementwise"][i].max()))
+        print(f"{what}: per-coefficient {pc:.2e} (bar {pbar:.2e}), elementwise {ew:.2e} (bar {bar:.2e})")
         assert ew <= bar, f"{what}: elementwise {ew:.3e} > bar {bar:.3e} (fp32 pocketfft x2 or 1e-5)"

@@ -145,6 +145,16 @@ def test_oracle_reproduces_golden(name):
     np.testing.assert_allclose(S.astype(np.float32), d["S"], rtol=2e-6, atol=1e-9)
 
 
+def test_oracle_reproduces_pattern_golden():
+    """The c5-geometry structured-pattern fixture (tests/golden/make_pattern_golden.py) is the
+    oracle's output: re-run one plane (the impulse, ~4 s)."""
+    d = load_golden("c5_patterns_256_J6_L12")
+    names = [str(n) for n in d["names"]]
+    i = names.index("impulse")
+    S = kr.Scattering2D(J=int(d["J"]), shape=d["x"].shape[-2:], L=int(d["L"]))(d["x"][i:i + 1])
+    np.testing.assert_allclose(S[0].astype(np.float32), d["S"][i], rtol=2e-6, atol=1e-9)
+
+
 def test_real_data_magnitude_sanity():
     # SURVEY §4.3: real 128^2 patches (J=2, L=8) have mean S0 ~ 0.5-0.63, S1 ~ 5e-3, S2 ~ 5e-4.
     # A uniform-noise 64^2 patch must land in the same decades for S0 and be non-trivial for S1/S2.

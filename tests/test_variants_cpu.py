@@ -3,8 +3,8 @@
 The library's host mirror of the kernels' run-time dispatch (wst_describe_variants, a plan built
 without a GPU) names, per launch, the kernel instantiation, the body it dispatches to and the
 branch of every order-2 level (wst_amd.variants).  tools/variant_cover.py walked a sweep of
-33k geometries in padded-size space (every square P to 584 and a grid to 1204, J 1..8, L 1..12,
-orders 1 and 2, rectangular pairs) and
+33k geometries in padded-size space (every square P to 584 and a grid to 1204, J 1..8,
+L in {1, 2, 3, 7, 8, 12}, orders 1 and 2; rectangular pairs with J 1..5, L in {3, 8}) and
 stored the reachable set in tests/golden/variant_universe.json; tests/variant_geometries.py is
 a cover of it, which tests/test_gpu_variants.py runs on the GPU against the float64 oracle and
 checks the device trace against the mirror.  Here:
@@ -12,7 +12,10 @@ checks the device trace against the mirror.  Here:
   * a fresh sweep reaches nothing outside the stored set (a code change that adds a variant
     fails here until the cover is regenerated);
   * the library compiles exactly the reachable k_o1 / k_o2 / k_prep / staged instantiations
-    (csrc/wst_compiled.h, generated from the same sweep).
+    (csrc/wst_compiled.h, generated from the same sweep);
+  * a seeded random sweep OFF that grid (L in 4..16 outside the grid's values, rectangular planes
+    with J up to 8) selects only compiled kernels: no plan fails with "not compiled", and every
+    kernel it names is in the library (guards a dispatch change that only affects off-grid L / J).
 """
 import json
 import os
@@ -20,6 +23,7 @@ import re
 import shutil
 import subprocess
 
+import numpy as np
 import pytest
 
 import wst_amd  # noqa: F401
@@ -94,3 +98,38 @@ def test_compiled_kernels_are_exactly_the_reachable_ones():
     compiled = _compiled_kernels()
     reached = {k.split(" [")[0] for k in UNIVERSE["keys"]}
     assert compiled == reached, (sorted(compiled - reached)[:5], sorted(reached - compiled)[:5])
+
+
+def _offgrid_geometries(n=1500, seed=6):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        J = int(rng.integers(1, 9))
+        s = 1 << J
+        L = int(rng.choice([4, 5, 6, 9, 10, 11, 13, 14, 15, 16]))
+        mo = int(rng.integers(1, 3))
+        hi = 1204 // s
+        PM = s * int(rng.integers(3, hi + 1))
+        PN = PM if rng.random() < 0.4 else s * int(rng.integers(3, hi + 1))
+        out.append((PM - 2 * s, PN - 2 * s, J, L, mo))
+    return out
+
+
+def _describe_or_error(g):
+    try:
+        return g, sorted(variants.variant_keys(_lib.describe_variants(*g))), None
+    except _lib.WSTError as e:
+        return g, None, str(e)
+
+
+def test_offgrid_geometries_select_only_compiled_kernels():
+    import multiprocessing as mp
+    with mp.get_context("fork").Pool(min(8, os.cpu_count() or 1)) as pool:
+        res = pool.map(_describe_or_error, _offgrid_geometries(), chunksize=32)
+    uncompiled = [(g, e) for g, _, e in res if e and "not compiled" in e]
+    assert not uncompiled, f"{len(uncompiled)} off-grid geometries hit an uncompiled kernel, e.g. {uncompiled[:2]}"
+    compiled = _compiled_kernels()
+    named = {k.split(" [")[0] for _, keys, _ in res if keys for k in keys}
+    assert named <= compiled, sorted(named - compiled)[:5]
+    valid = sum(keys is not None for _, keys, _ in res)
+    assert valid > 500, valid     # the sweep mostly reaches plannable geometries

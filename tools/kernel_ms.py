@@ -31,4 +31,6 @@ for chunk in [int(a) for a in sys.argv[1:]] or [2048]:
     acc = [round(a / 5, 3) for a in acc]
     print(os.environ.get("AB_LIB", "default"), f"chunk={chunk} wall={wall:.3f} ms",
           "prep", acc[0], "o1", acc[1:1 + J], "o2", acc[1 + J:], "sum", round(sum(acc), 3), flush=True)
+    if os.environ.get("KM_DUMP"):   # the outputs of the first 64 planes, for a cross-library check
+        np.save(os.environ["KM_DUMP"], out[:64].cpu().numpy())
     del ws

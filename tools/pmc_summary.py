@@ -9,8 +9,15 @@ for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=T
         if "rocclr" in name:
             continue
         short = name.replace("void (anonymous namespace)::", "").split("(")[0]
-        agg[short][r["Counter_Name"]] += float(r["Counter_Value"])
+        # counters that appear in several passes (SQ_WAVES, SQ_BUSY_CYCLES) are kept per pass file
+        # and averaged below, not summed over the passes
+        agg[short][(r["Counter_Name"], f)] += float(r["Counter_Value"])
         disp[short].add(r["Dispatch_Id"])
+for k in agg:
+    per = collections.defaultdict(list)
+    for (n, f), v in agg[k].items():
+        per[n].append(v)
+    agg[k] = {n: sum(v) / len(v) for n, v in per.items()}
 for k in sorted(agg):
     c = agg[k]
     w = c.get("SQ_WAVES", 0) or 1
@@ -23,3 +30,8 @@ for k in sorted(agg):
               f"add {c.get('SQ_INSTS_VALU_ADD_F32',0)/v:.2%} mul {c.get('SQ_INSTS_VALU_MUL_F32',0)/v:.2%}")
     if "SQ_LDS_BANK_CONFLICT" in c and c.get("SQ_LDS_IDX_ACTIVE"):
         print(f"   LDS conflict cycles / LDS active: {c['SQ_LDS_BANK_CONFLICT']/c['SQ_LDS_IDX_ACTIVE']:.2%}")
+    if c.get("SQ_WAVE_CYCLES"):
+        wc = c["SQ_WAVE_CYCLES"]
+        print("   share of wave cycles: " + " ".join(
+            f"{n[3:].lower()} {c[n] / wc:.2%}" for n in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_INST_LDS",
+                                                       "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU") if n in c))

@@ -56,6 +56,13 @@ constexpr int kWholeFirstCap = 24;
 // 512 threads.  The columns keep split_n2 (grouped column partials); the S2 pass reads each
 // logical column's partial from its position in the rows' order (cols_modlp RS).
 constexpr int fused_row_n2(int n) { return n == 48 ? 8 : 0; }
+// Column split of the fused column pass + |.| + S2 (cols_modlp; 0: split_n2).  The tap matrices GM
+// are built for split_n2's digit-reversed row order; another split reads each physical row's taps
+// from that row's position in split_n2's order (cols_modlp, needs split_n2's N1 divisible by its N1).
+#ifndef WST_COL48_N2   // A/B builds (tools/variant.sh -DWST_COL48_N2=n)
+#define WST_COL48_N2 12
+#endif
+constexpr int fused_col_n2(int n) { return n == 48 ? WST_COL48_N2 : 0; }
 
 
 constexpr int kMaxLds = 160 * 1024;
@@ -775,12 +782,15 @@ __device__ __forceinline__ void lds_lowpass_mfma_rc(float2* U, int nb, int bs, i
     // 1. T = U GN: every wave keeps one column tile (waves w and w + nnt share it, splitting its
     //    row tiles).  Needs nw >= nnt: the plan checks it for every launch that takes this form
     //    (wst_hip.hip, rc_waves_ok).  (A
-    //    nested loop serving nw < nnt here cost the f3 k_o2 1.8 %, measured round 5.)
-    {
+    //    nested loop serving nw < nnt here cost the f3 k_o2 1.8 %, measured round 5.)  Should a
+    //    launch break it anyway, the stride stays >= 1 (wrong maps, never a hang); waves beyond the
+    //    last whole group of nnt would only repeat other waves' tiles and skip step 1.
+    const int tstep = nw >= nnt ? nw / nnt : 1;
+    if (wave < nnt * tstep || nw < nnt) {
         float g[KS];
         const int nt = wave % nnt;
         load_ops(GN, nnt, nt, g);
-        for (int tk = wave / nnt; tk < nb * NMT; tk += nw / nnt) {
+        for (int tk = wave / nnt; tk < nb * NMT; tk += tstep) {
             const int b = tk / NMT, mt = tk - b * NMT;
             float2* Ub = U + b * bs;
             const int p = mt * 16 + li;
@@ -951,10 +961,17 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
                                            const float2* tw, const float* GM, const float* GN,
                                            int oms, int oM, int oN, float scale, float* S,
                                            float* outd) {
-    using F = wstfft::LineFFT<NN, true>;
+    using F = wstfft::LineFFT<NN, true, fused_col_n2(NN)>;
+    using FS = wstfft::LineFFT<NN, true>;    // the split GM's rows are ordered for
     constexpr bool single = (F::N2 == 1);
     constexpr int RU = single ? NN : F::N2;  // rows per unit
     constexpr int NU = single ? 1 : F::N1;   // units per column
+    // remap: physical row RU k + e holds logical row k + NU e, whose taps sit in GM row
+    // FS::N2 (k + NU t) + m (e = RR m + t, RR = FS::N1 / NU): a per-unit base plus a per-e constant
+    constexpr bool remap = !single && F::N2 != FS::N2;
+    static_assert(!remap || (FS::N2 > 1 && FS::N1 % F::N1 == 0), "column split must refine split_n2's N1");
+    constexpr int RR = remap ? FS::N1 / F::N1 : 1;
+    constexpr int GU = remap ? FS::N2 : RU;  // GM rows per unit step k
     // grouped: the NU units of a column sit in NU adjacent lanes and their partials are summed
     // there (DPP), so the S pass reads one partial per column instead of NU
     constexpr bool grouped = !single && (NU & (NU - 1)) == 0 && NU <= 16;
@@ -979,7 +996,7 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
             v[e] = p[e * ld];
         });
         wstfft::rfft<RU, true>(v);
-        const float* gm = GM + (RU * k) * oms;
+        const float* gm = GM + (GU * k) * oms;
         if constexpr (single) {
             // whole column in one unit: the tap loads of a rolled loop over output-row pairs keep
             // the register footprint to the RU moduli (unrolled, the RU x oms GM loads hoist)
@@ -1007,13 +1024,14 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
         wstfft::static_for<0, RU>([&](auto ec) {
             constexpr int e = decltype(ec)::value;
             const float m = __builtin_amdgcn_sqrtf(fmaf(v[e].x, v[e].x, v[e].y * v[e].y)) * scale;
-            const float4 g0 = *reinterpret_cast<const float4*>(gm + e * oms);
+            constexpr int ge = remap ? FS::N2 * NU * (e % RR) + e / RR : e;
+            const float4 g0 = *reinterpret_cast<const float4*>(gm + ge * oms);
             V[0] = fmaf(g0.x, m, V[0]);
             V[1] = fmaf(g0.y, m, V[1]);
             V[2] = fmaf(g0.z, m, V[2]);
             V[3] = fmaf(g0.w, m, V[3]);
             if (oM > 4) {
-                const float4 g1 = *reinterpret_cast<const float4*>(gm + e * oms + 4);
+                const float4 g1 = *reinterpret_cast<const float4*>(gm + ge * oms + 4);
                 V[4] = fmaf(g1.x, m, V[4]);
                 V[5] = fmaf(g1.y, m, V[5]);
                 V[6] = fmaf(g1.z, m, V[6]);

@@ -332,6 +332,10 @@ constexpr size_t kMaxStreamWs = 4;   // streams that keep an internal workspace 
 
 // paths per order-2 batch at level j2 (mirrors k_o2)
 constexpr int kHgSplit = 1;   // k_o2 HG workgroups per (plane, theta1) (4 until round 5)
+#ifndef WST_STAGED_WS_GB   // A/B builds only (tools/variant.sh HOST_ONLY=1 -DWST_STAGED_WS_GB=...)
+#define WST_STAGED_WS_GB 2
+#endif
+constexpr size_t kStagedWsBytes = size_t(WST_STAGED_WS_GB) << 30;   // staged plans: chunk workspace cap
 constexpr int kHgGroup = 16;  // k_o2 HG items per batch-major dispatch group of an XCD
 
 int paths_per_batch(size_t bcap, size_t pslot, int L) {
@@ -348,10 +352,17 @@ int rows_per_unit(int n) {
 
 // Bins of a filter (pair) below this fraction of the filter's maximum are skipped by the box-sparse
 // folds.  Zeroing every psi bin below it moves the float64 oracle's coefficients by at most
-// 1.7e-8 (64^2 J=4), 5.3e-9 (128^2 J=2), 2.5e-8 (256^2 J=6 L=12) of each coefficient's maximum --
-// below fp32 resolution (6e-8) and 400x below the 1e-5 parity bar (tools/box_threshold.py;
-// 1e-10, the round-1..4 value, kept 11 % more bins at c5).
-constexpr double kBoxThreshold = 1e-8;
+// 1.7e-8 (64^2 J=4), 5.3e-9 (128^2 J=2), 2.5e-8 (256^2 J=6 L=12) of each coefficient's maximum on
+// random planes, and at c5's geometry on the structured patterns by at most 3.4e-7 (edge; 2.5e-8
+// impulse / checkerboard / gradients) per coefficient and 3.1e-5 elementwise on the significant
+// entries (edge, whose fp32 noise floor is 2.2e-3) -- 30x below the 1e-5 parity bar
+// (tests/golden/box_threshold.py, profiles/r06_box_threshold_patterns.txt; GPU:
+// tests/test_gpu_patterns.py::test_structured_patterns_c5_geometry).  1e-10, the round-1..4
+// value, kept 11 % more bins at c5.
+#ifndef WST_BOX_THR   // A/B builds only (tools/variant.sh HOST_ONLY=1 -DWST_BOX_THR=...)
+#define WST_BOX_THR 1e-8
+#endif
+constexpr double kBoxThreshold = WST_BOX_THR;
 
 // Minimal cyclic window [i0, i0 + n) of Z_s covering the set bits of `hit` -> i0 | n << 8.
 int cyclic_window(const std::vector<char>& hit) {
@@ -953,6 +964,12 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
         tmp_c = std::max(tmp_c, static_cast<size_t>(L) * m1 * n1);
         part_n = std::max(part_n, static_cast<size_t>(L) * n1);
         if (!do2) continue;
+        // kRowHalf derives the spectrum height from its half-row count (m = 2 (rows - 1)) and
+        // writes row m - k as the mirror of row k: both hold only for an even m (padding to
+        // multiples of 2^J makes every staged level with order 2 even; checked, not assumed)
+        if (m1 % 2 != 0 || n1 % 2 != 0)
+            return fail(WST_ERR_UNSUPPORTED, "staged order-2 level " + std::to_string(j1) + " (" +
+                                                 std::to_string(m1) + "x" + std::to_string(n1) + ") must be even");
         plan->ws_hbig[j1] = wsp;
         wsp += align16(static_cast<size_t>(L) * m1 * (n1 / 2 + 1) * sizeof(float2));
         // column spectra of U1, rows 0..m1/2 (kColModLpFwd -> kRowHalf)
@@ -1063,8 +1080,8 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
         plan->o1_lay[j1].hext = plan->o2_lay[j1].hext = 1;
     }
     plan->ws_plane = align16(wsp);
-    if (plan->rb > 0)   // staged plans hold ~tens of MB per plane: bound the chunk to ~2 GB
-        plan->max_chunk = std::max<int64_t>(1, std::min<int64_t>(2048, (size_t(2) << 30) / plan->ws_plane));
+    if (plan->rb > 0)   // staged plans hold ~tens of MB per plane: bound the chunk's workspace
+        plan->max_chunk = std::max<int64_t>(1, std::min<int64_t>(2048, kStagedWsBytes / plan->ws_plane));
     if (std::getenv("WST_VERBOSE")) {
         std::fprintf(stderr, "[wst] plan %dx%d J=%d L=%d P=%dx%d fam=(%d,%d) sq=%d prep_lds=%zu\n", M, N, J, L,
                      g.PM, g.PN, plan->fam_m, plan->fam_n, plan->sq, plan->prep_lds);
@@ -1879,10 +1896,19 @@ int wst_plan_trace(wst_plan* plan, int enable) {
         return fail(WST_ERR_UNSUPPORTED, "this library has no trace code: the variant trace is in "
                                          "libwst_hip_trace.so (same sources, -DWST_TRACE)");
 #endif
+    // The trace switch changes the kernel parameters every later launch copies and clears the
+    // trace area: it needs a quiescent plan.  Calls that overlap forwards on other host threads are
+    // serialised against their launches (ws_mu), and the device is drained first, so no launch in
+    // flight writes the area being cleared (header: wst_plan_trace).
+    std::lock_guard<std::mutex> lk(plan->ws_mu);
+    WST_HIP_CHECK(hipDeviceSynchronize());
     if (!enable) {
         plan->dp.flags &= ~kFlagTrace;
         return WST_OK;
     }
+    if (describe_chunk(plan).size() > static_cast<size_t>(kTraceSites) * kTraceW)
+        return fail(WST_ERR_UNSUPPORTED, "plan has more launch sites per chunk than the trace holds (" +
+                                             std::to_string(kTraceSites) + ")");
     const size_t bytes = static_cast<size_t>(kTraceSites) * kTraceW * sizeof(int);
     WST_HIP_CHECK(hipMemset(plan->d_o2 + static_cast<size_t>(plan->g.J) * plan->g.L, 0, bytes));
     plan->dp.flags |= kFlagTrace;
@@ -1892,8 +1918,9 @@ int wst_plan_trace(wst_plan* plan, int enable) {
 int wst_plan_read_trace(const wst_plan* plan, int32_t* out, int64_t max_words, int64_t* nwords) {
     if (!plan || !out || !nwords) return fail(WST_ERR_INVALID, "plan/out/nwords is NULL");
     if (!(plan->dp.flags & kFlagTrace)) return fail(WST_ERR_INVALID, "tracing is off (wst_plan_trace)");
-    const int64_t n = std::min<int64_t>(static_cast<int64_t>(describe_chunk(plan).size()),
-                                        static_cast<int64_t>(kTraceSites) * kTraceW);
+    const int64_t n = static_cast<int64_t>(describe_chunk(plan).size());
+    if (n > static_cast<int64_t>(kTraceSites) * kTraceW)   // never truncated to a shape unlike the mirror's
+        return fail(WST_ERR_UNSUPPORTED, "plan has more launch sites per chunk than the trace holds");
     if (max_words < n) return fail(WST_ERR_INVALID, "output buffer too small");
     WST_HIP_CHECK(hipDeviceSynchronize());
     WST_HIP_CHECK(hipMemcpy(out, plan->d_o2 + static_cast<size_t>(plan->g.J) * plan->g.L,
