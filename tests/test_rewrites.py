@@ -34,19 +34,21 @@ def test_kernel_dataflow_equals_kymatio_cascade(M, N, J, L):
 
 @pytest.mark.parametrize("nM,nN,s", [(96, 96, 2), (48, 48, 4), (24, 40, 2), (136, 136, 2), (12, 12, 2)])
 def test_half_spectrum_pack_split_and_hermitian_fold(nM, nN, s):
-    """k_o1/k_o2 rewrite of fft2(U1) and the order-2 fold (wst_device.h): two real rows packed as
-    re/im of one complex row, one row FFT, split into the rows' half spectra (columns 0..nN/2);
+    """k_o1/k_o2 rewrite of fft2(U1) and the order-2 fold (wst_device.h): two real rows (r and
+    r + nM/2, k_o1 step 4) packed as re/im of one complex row, one row FFT, split into the rows'
+    half spectra (columns 0..nN/2);
     the column FFT of the half spectrum; the fold reading columns > nN/2 through Hermitian
     symmetry U1hat[kr][kc] = conj(U1hat[-kr][nN-kc])."""
     rng = np.random.default_rng(nM + nN)
     U = rng.random((nM, nN))
-    Z = np.fft.fft(U[0::2] + 1j * U[1::2], axis=1)
+    nh = nM // 2
+    Z = np.fft.fft(U[:nh] + 1j * U[nh:], axis=1)
     Zm = Z[:, (-np.arange(nN)) % nN]
     hld = nN // 2 + 1
     Xa = (0.5 * (Z + np.conj(Zm)))[:, :hld]
     Xb = (-0.5j * (Z - np.conj(Zm)))[:, :hld]
     H = np.empty((nM, hld), complex)
-    H[0::2], H[1::2] = Xa, Xb
+    H[:nh], H[nh:] = Xa, Xb
     # kernel arithmetic of the split: Xa=((z.x+zm.x)/2,(z.y-zm.y)/2), Xb=((z.y+zm.y)/2,-(z.x-zm.x)/2)
     z, zm = Z[:, :hld], Zm[:, :hld]
     np.testing.assert_allclose(Xa, 0.5 * (z.real + zm.real) + 0.5j * (z.imag - zm.imag), atol=1e-12)

@@ -63,6 +63,9 @@ constexpr int fused_row_n2(int n) { return n == 48 ? 8 : 0; }
 #define WST_COL48_N2 12
 #endif
 constexpr int fused_col_n2(int n) { return n == 48 ? WST_COL48_N2 : 0; }
+#ifndef WST_O1_PACK_HALF   // A/B builds (tools/variant.sh -DWST_O1_PACK_HALF=0: k_o1 packs rows 2r, 2r + 1)
+#define WST_O1_PACK_HALF 1
+#endif
 
 
 constexpr int kMaxLds = 160 * 1024;
@@ -1954,24 +1957,29 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
     }
     if (!do2) return;
 
-    // 4. real-input row FFT of (U1 - mean): physical rows 2r, 2r+1 packed as re/im of row 2r
-    //    (packing inside the transform's first stage measured neutral: c2 k_o1 0.728 -> 0.727 ms)
+    // 4. real-input row FFT of (U1 - mean): physical rows r, r + nh packed as re/im of row r
+    //    (packing inside the transform's first stage measured neutral: c2 k_o1 0.728 -> 0.727 ms).
+    //    Rows r and r + nh rather than 2r and 2r + 1: the packed lines keep the odd row stride, so
+    //    the transform's lane groups do not meet 2-way bank conflicts (stride 2 ld1: 4 banks apart)
     const int nh = nM1 >> 1;
+    constexpr int PK = WST_O1_PACK_HALF;   // 1: rows (r, r + nh); 0: rows (2r, 2r + 1) (A/B builds)
+    const int prow = PK ? 1 : 2;           // packed line r sits at row prow * r
+    const int pmate = PK ? nh : 1;         // its imaginary part's row, relative to it
     for (GridIter it(nN1); it.u < nh; it.next()) {
-        float2* a = A + (2 * it.u) * ld1 + it.v;
-        *a = make_float2(a->x - mean1, a[ld1].x - mean1);
+        float2* a = A + (prow * it.u) * ld1 + it.v;
+        *a = make_float2(a->x - mean1, a[pmate * ld1].x - mean1);
     }
     __syncthreads();
     wstfft::EpiIdentity id;
     if (!(dbg & 4))
-        lds_fft_lines<FN, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(A, wstfft::Lines{1, 0, nh, 2 * ld1, 1}, nN1,
+        lds_fft_lines<FN, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(A, wstfft::Lines{1, 0, nh, prow * ld1, 1}, nN1,
                                             tb.twN(j1), id);
 
     // 5. split into the two rows' half spectra (columns 0..nN1/2) and export them
     const int hld = (nN1 >> 1) + 1;
     float2* H = hexp + item * hspec_stride(nM1, hld, lay.hext);
     if (export_full(lay)) {
-        // in place: packed row 2t -> half-spectrum rows 2t and 2t+1 (the odd rows of A are free),
+        // in place: packed row t -> half-spectrum rows t and t + nh (rows nh.. of A are free),
         // then the column FFTs (rows digit-reversed -> natural); k_o2 folds the fully transformed
         // spectrum from HBM/L2 and keeps only its path batches in LDS (host: nh * hld <= KS * T)
         constexpr int KS = 8;
@@ -1985,12 +1993,12 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
             dst[k] = -1;
             if (w < nitems) {
                 const int t = dh.div(w), v = w - t * hld;
-                const float2* row = A + (2 * t) * ld1;
+                const float2* row = A + (prow * t) * ld1;
                 const float2 z = row[v];
                 const float2 zm = row[v == 0 ? 0 : nN1 - v];
                 e0[k] = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
                 e1[k] = make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
-                dst[k] = (2 * t) * ld1 + v;
+                dst[k] = (prow * t) * ld1 + v;
             }
         }
         __syncthreads();
@@ -1998,7 +2006,7 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
         for (int k = 0; k < KS; ++k)
             if (dst[k] >= 0) {
                 A[dst[k]] = e0[k];
-                A[dst[k] + ld1] = e1[k];
+                A[dst[k] + pmate * ld1] = e1[k];
             }
         __syncthreads();
         lds_fft_lines<FM, SQ ? prev_cap(MAXN) : 0, MAXN, kRD, false>(A, wstfft::Lines{1, 0, hld, 1, ld1}, nM1,
@@ -2009,14 +2017,14 @@ __device__ __forceinline__ void k_o1_body(unsigned char* smem, const DevParams& 
         return;
     }
     for (GridIter it(hld); it.u < nh; it.next()) {
-        const float2* row = A + (2 * it.u) * ld1;
+        const float2* row = A + (prow * it.u) * ld1;
         const float2 z = row[it.v];
         const float2 zm = row[it.v == 0 ? 0 : nN1 - it.v];
         const float2 h0 = make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y));
         const float2 h1 = make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x));
-        float2* d = H + (2 * it.u) * hld + it.v;
+        float2* d = H + (prow * it.u) * hld + it.v;
         stnt(d, h0);
-        stnt(d + hld, h1);
+        stnt(d + pmate * hld, h1);
     }
 }
 

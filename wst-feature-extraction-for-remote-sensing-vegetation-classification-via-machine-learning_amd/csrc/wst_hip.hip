@@ -333,9 +333,12 @@ constexpr size_t kMaxStreamWs = 4;   // streams that keep an internal workspace 
 // paths per order-2 batch at level j2 (mirrors k_o2)
 constexpr int kHgSplit = 1;   // k_o2 HG workgroups per (plane, theta1) (4 until round 5)
 #ifndef WST_STAGED_WS_GB   // A/B builds only (tools/variant.sh HOST_ONLY=1 -DWST_STAGED_WS_GB=...)
-#define WST_STAGED_WS_GB 2
+#define WST_STAGED_WS_GB 8
 #endif
-constexpr size_t kStagedWsBytes = size_t(WST_STAGED_WS_GB) << 30;   // staged plans: chunk workspace cap
+// Staged plans: chunk workspace cap.  c5 holds 31.5 MB per plane: 8 GB (of 288 GB HBM) runs BASELINE
+// config 5's 256 planes as one chunk, every staged launch over all of them (22.19 -> 20.85-20.91 ms
+// per step against 2 GB = 4 chunks of 64; 4 GB: 21.25; profiles/r06_ab.txt r06e)
+constexpr size_t kStagedWsBytes = size_t(WST_STAGED_WS_GB) << 30;
 constexpr int kHgGroup = 16;  // k_o2 HG items per batch-major dispatch group of an XCD
 
 int paths_per_batch(size_t bcap, size_t pslot, int L) {
