@@ -55,10 +55,7 @@ constexpr int kWholeFirstCap = 24;
 // 48 = 6 x 8 gives the fused phase 384 units of 6 elements per filter pair instead of 288 of 8 on
 // 512 threads.  The columns keep split_n2 (grouped column partials); the S2 pass reads each
 // logical column's partial from its position in the rows' order (cols_modlp RS).
-#ifndef WST_ROW48_N2   // A/B builds (tools/variant.sh -DWST_ROW48_N2=n)
-#define WST_ROW48_N2 8
-#endif
-constexpr int fused_row_n2(int n) { return n == 48 ? WST_ROW48_N2 : 0; }
+constexpr int fused_row_n2(int n) { return n == 48 ? 8 : 0; }
 // Column split of the fused column pass + |.| + S2 (cols_modlp; 0: split_n2).  The tap matrices GM
 // are built for split_n2's digit-reversed row order; another split reads each physical row's taps
 // from that row's position in split_n2's order (cols_modlp, needs split_n2's N1 divisible by its N1).
@@ -962,21 +959,11 @@ typedef __attribute__((address_space(3))) float* lfloat_p;
 typedef const __attribute__((address_space(1))) float* gcfloat_p;
 typedef const __attribute__((address_space(3))) float* lcfloat_p;
 
-// Direct S2 contraction (DS, the fused 48-point rows of the 4 x 4-map headline with 4 x 12 columns):
-// lane k of a column's unit group multiplies the column's W[a] by GN[q][k] (oN = NU = 4), the four
-// column groups of a 16-lane row are summed by DPP rotations and the row partials go to P
-// (2 paths x 16 outputs x 12 rows); the 12 partials of an output are summed after stage B's barrier
-// by 128 threads, and no separate S pass (nor its barrier) runs.
-#ifndef WST_DIRECT_S2   // A/B builds (tools/variant.sh -DWST_DIRECT_S2=1)
-#define WST_DIRECT_S2 0
-#endif
-constexpr int kDsRows = 12;   // 16-lane rows (4 columns each) per 48-column path
-constexpr int kDsOut = 32;    // S floats before P (2 paths x 16 outputs); host: S area >= kDsOut + 2 x 16 x kDsRows
 template <int NN, int RS = 0>
 __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, int ld,
                                            const float2* tw, const float* GM, const float* GN,
                                            int oms, int oM, int oN, float scale, float* S,
-                                           float* outd, float* P = nullptr) {
+                                           float* outd) {
     using F = wstfft::LineFFT<NN, true, fused_col_n2(NN)>;
     using FS = wstfft::LineFFT<NN, true>;    // the split GM's rows are ordered for
     constexpr bool single = (F::N2 == 1);
@@ -992,8 +979,6 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
     // there (DPP), so the S pass reads one partial per column instead of NU
     constexpr bool grouped = !single && (NU & (NU - 1)) == 0 && NU <= 16;
     constexpr int NUS = grouped ? 1 : NU;    // partials per column left for the S pass
-    constexpr bool DS = WST_DIRECT_S2 && grouped && NU == 4 && NN == 48 && RS > 0;
-    const bool ds = DS && P && oM == 4 && oN == 4 && oms == 4 && cols == NN;
     const wstfft::Lines g(nb, bs, cols, 1, ld);
     const int T = blockDim.x;
     const int nlines = nb * cols;
@@ -1060,29 +1045,6 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
 #pragma unroll
             for (int a = 0; a < kLpOM; ++a)
                 if (a < oM) V[a] = group_sum<NU>(V[a]);
-            if constexpr (DS) {
-                if (ds) {
-                    // physical column qp (rows' order RS) -> its GN row (split_n2 order)
-                    constexpr int N2d = wstfft::split_n2(NN), N1d = NN / N2d, N1r = NN / RS;
-                    const int b = line / NN, qp = line - b * NN;
-                    const int lg = N1r * (qp % RS) + qp / RS;
-                    const int qg = N2d * (lg % N1d) + lg / N1d;
-                    const float gk = GN[qg * 4 + k];
-                    float Pa[4];
-#pragma unroll
-                    for (int a = 0; a < 4; ++a) {
-                        Pa[a] = gk * V[a];
-                        Pa[a] += dpp_mov<0x124>(Pa[a]);   // row_ror:4
-                        Pa[a] += dpp_mov<0x128>(Pa[a]);   // row_ror:8
-                    }
-                    if ((threadIdx.x & 15) < 4) {
-#pragma unroll
-                        for (int a = 0; a < 4; ++a)
-                            ((lfloat_p)P)[((b * 4 + a) * 4 + k) * kDsRows + (qp >> 2)] = Pa[a];
-                    }
-                    continue;
-                }
-            }
             if (k != 0) continue;
         }
 #pragma unroll
@@ -1090,26 +1052,6 @@ __device__ __forceinline__ void cols_modlp(float2* U, int nb, int bs, int cols, 
             if (2 * t < oM) p[t * ld] = make_float2(V[2 * t], V[2 * t + 1]);
     }
     __syncthreads();
-    if constexpr (DS) {
-        if (ds) {
-            // 4 lanes per output (b, a, c), 3 of its 12 row partials each; no barrier after: the next
-            // fold writes B only, and P is rewritten only after that batch's transform barriers
-            const int nout = nb * 16;
-            const int w = threadIdx.x;
-            if (w < nout * 4) {
-                const int o = w >> 2, part = w & 3;
-                const lfloat_p pr = (lfloat_p)P + o * kDsRows + 3 * part;
-                float acc = pr[0] + pr[1] + pr[2];
-                acc = group_sum<4>(acc);
-                if (part == 0) {
-                    if (outd) __builtin_nontemporal_store(acc, (gfloat_p)outd + o);
-                    else ((lfloat_p)S)[o] = acc;
-                }
-            }
-            if (!outd) __syncthreads();   // emit reads S
-            return;
-        }
-    }
     // 2+3. S = (sum_k V_k) GN in one pass: QC lanes split the columns q of output (b, a, c), each
     //      sums the NU unit partials of its columns, shuffle reduction.  outd (nullable): write
     //      S straight to the coefficient maps instead of S (non-pooled output).
@@ -1161,17 +1103,17 @@ template <int FAM, int K, int HI, int RS = 0>
 __device__ __forceinline__ void family_cols_modlp(float2* U, int nb, int bs, int rows, int cols,
                                                   int ld, const float2* tw, const float* GM,
                                                   const float* GN, int oms, int oM, int oN,
-                                                  float scale, float* S, float* outd, float* P = nullptr) {
+                                                  float scale, float* S, float* outd) {
     constexpr int NN = FAM << K;
     if constexpr (FAM > 0 && NN <= HI && NN <= wstfft::kMaxFamilyN) {
         // RS > 0 belongs to the fused 48-point rows only: no other size is compiled for it
         if constexpr (NN >= 2 && (RS == 0 || fused_row_n2(NN) == RS)) {
             if (rows == NN) {
-                cols_modlp<NN, RS>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd, P);
+                cols_modlp<NN, RS>(U, nb, bs, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
                 return;
             }
         }
-        family_cols_modlp<FAM, K + 1, HI, RS>(U, nb, bs, rows, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd, P);
+        family_cols_modlp<FAM, K + 1, HI, RS>(U, nb, bs, rows, cols, ld, tw, GM, GN, oms, oM, oN, scale, S, outd);
     }
 }
 
@@ -2301,7 +2243,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                     family_cols_modlp<FM, 0, PHI, FUSE ? fused_row_n2(N1F > 0 ? N1F / 2 : 2) : 0>(
                                                        B, npath, pslot, nM2, nN2, ld2, tb.twM(j2),
                                                        tb.gM(j2), tb.gN(j2), oms, oM, oN,
-                                                       scale2, S, outd, FUSE && npath <= 2 ? S + kDsOut : nullptr);
+                                                       scale2, S, outd);
                 if (!outd) emit(S, npath, k0, img, p.K, oM, oN, out, pooled);
             } else {
                 EpiModulus mod2{scale2, 0.f};

@@ -1070,8 +1070,6 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
         size_t smax = 0;
         for (int j2 = j1 + 1; j2 < J; ++j2)
             smax = std::max(smax, static_cast<size_t>(paths_per_batch(bcap, pslot(j2), L)) * omn);
-        if (WST_DIRECT_S2 && plan->sq && nM1 == 96 && nN1 == 96 && omn == 16)   // cols_modlp's P
-            smax = std::max(smax, static_cast<size_t>(wstdev::kDsOut + 2 * 16 * wstdev::kDsRows));
         if (plan->sq)   // tap matrices replace the 1-D taps and permutations; M-side tables only;
                         // H holds row nM1 = row 0 (the tile folds' mirrored taps)
             plan->o2_lds[j1] = layout(plan->o2_lay[j1], static_cast<size_t>(nM1 + 1) * hld * sizeof(float2),
@@ -1126,8 +1124,6 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
         size_t smax = 0;
         for (int j2 = j1 + 1; j2 < J; ++j2)
             smax = std::max(smax, static_cast<size_t>(paths_per_batch(bcap, pslot(j2), L)) * omn);
-        if (WST_DIRECT_S2 && plan->sq && nM1 == 96 && nN1 == 96 && omn == 16)   // cols_modlp's P
-            smax = std::max(smax, static_cast<size_t>(wstdev::kDsOut + 2 * 16 * wstdev::kDsRows));
         // wide maps are written into the path arrays themselves (no S region); square: M-side
         // twiddle tables serve both dimensions
         const size_t lds =
