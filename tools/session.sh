@@ -6,7 +6,7 @@
 #   pytest[=<file>]                     GPU tests (all of -m gpu, or one test file)
 #   ab=<geom>:<reps>:<lib>[,<lib>...]   alternating per-kernel HIP-event A/B of library builds in the
 #                                       package dir (tools/ab_rep.sh); geom = planes,M,J[,L]
-#   env=<name>:<lib>:<geom>[:VAR=v,...] per-kernel ms of one library under env settings (diagnostic
+#   env=<name>:<lib>:<geom>[:VAR=v+...] per-kernel ms of one library under env settings (diagnostic
 #                                       builds read WST_* knobs)
 #   km=<geom>:<chunk>[,<chunk>...][:<lib>]  per-kernel ms at several chunk sizes (planes per chunk)
 #   pat=<lib>[,<lib>...]               c5-geometry structured-pattern errors per build (tools/pattern_check.py)
@@ -32,7 +32,7 @@ for step in "$@"; do
       bash tools/ab_rep.sh ${tag} $geom $reps ${libs//,/ } || exit 99 ;;
     env)
       IFS=: read -r name lib geom vars <<< "$arg"
-      env ${vars//,/ } AB_LIB=$lib WST_KM_GEOM=$geom timeout -k 10 200 python3 tools/kernel_ms.py 1536 > $o/${tag}_$name.txt 2>&1 \
+      env ${vars//+/ } AB_LIB=$lib WST_KM_GEOM=$geom timeout -k 10 200 python3 tools/kernel_ms.py 1536 > $o/${tag}_$name.txt 2>&1 \
         || { echo "$name failed"; tail -3 $o/${tag}_$name.txt; exit 99; }
       echo "$name $(tail -1 $o/${tag}_$name.txt)" ;;
     km)
