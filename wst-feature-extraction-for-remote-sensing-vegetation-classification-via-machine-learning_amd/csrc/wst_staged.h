@@ -39,6 +39,44 @@ constexpr int big_col_threads(int n) { return n >= 384 ? 512 : 256; }
 constexpr int kColTile = 16;         // columns per column-pass workgroup (128 B rows)
 constexpr int kMeanParts = 16;                  // k_big_mean partial sums per plane
 constexpr int kLoadBatch = 8;                   // global loads per thread in flight (tile loads)
+#ifndef WST_TILE_BATCH_MAX   // A/B builds: column-tile loads per thread in flight (compiled lengths)
+#define WST_TILE_BATCH_MAX 16
+#endif
+#ifndef WST_ROW_BATCH        // A/B builds: kRowFold1 (s = 1) loads per thread in flight
+#define WST_ROW_BATCH 8
+#endif
+#ifndef WST_FOLD_PREFETCH    // A/B builds: fold_all loads the next pair's filter taps one pair ahead
+#define WST_FOLD_PREFETCH 0
+#endif
+#ifndef WST_ROW_BATCH_384    // A/B builds: kRowFold1 (s = 1) loads in flight at the 384-point level
+#define WST_ROW_BATCH_384 WST_ROW_BATCH
+#endif
+#ifndef WST_IN_BATCH         // A/B builds: kRowPad / kRowHalf / kRowFold1 (s = 2) loads in flight
+#define WST_IN_BATCH 1
+#endif
+#ifndef WST_FOLD_PG          // A/B builds: fold_all filter pairs whose taps are loaded together
+#define WST_FOLD_PG 1
+#endif
+#ifndef WST_WIDE_IO          // A/B builds: 16-byte (two-element) column-tile loads / fold_all stores
+#define WST_WIDE_IO 0
+#endif
+typedef float wst_f4 __attribute__((ext_vector_type(4)));
+// two consecutive complex elements as one 16-byte streaming load / store (16-byte aligned)
+__device__ __forceinline__ wst_f4 ldnt2(const float2* p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const wst_f4*>(p));
+}
+__device__ __forceinline__ void stnt2(float2* p, float2 a, float2 b) {
+    wst_f4 v = {a.x, a.y, b.x, b.y};
+    __builtin_nontemporal_store(v, reinterpret_cast<wst_f4*>(p));
+}
+// Column-tile loads per thread in flight: a compiled length's whole tile share (N x kColTile /
+// threads: 12 at 192 and 384) in one batch, up to WST_TILE_BATCH_MAX; runtime lengths kLoadBatch
+constexpr int col_tile_batch(int N) {
+    return N > 0 ? ((N * kColTile + big_col_threads(N) - 1) / big_col_threads(N) < WST_TILE_BATCH_MAX
+                        ? (N * kColTile + big_col_threads(N) - 1) / big_col_threads(N)
+                        : WST_TILE_BATCH_MAX)
+                 : kLoadBatch;
+}
 constexpr int kBigOGroup = 16;                  // outputs per accumulation round of wide low-passes
 
 enum RowMode { kRowPad = 0, kRowFold1 = 2, kRowFold2 = 3, kRowHalf = 4 };   // (1: retired)
@@ -134,12 +172,24 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
         // arr = chunk-local plane; raw values first (S0 partials), then mean-centred
         const int inM = p.pre_pad ? p.PM : p.M, inN = p.pre_pad ? p.PN : p.N;
         const float* x = a.in + static_cast<long long>(arr) * inM * inN;
-        for (int i = threadIdx.x; i < a.rows * n; i += T) {
-            const int rr = i / n, q = i - (i / n) * n;
-            const int u = r0 + rr;
-            const int su = p.pre_pad ? u : wstdev::reflect_index(u - p.padTop, p.M);
-            const int sv = p.pre_pad ? q : wstdev::reflect_index(q - p.padLeft, p.N);
-            A[rr * ld + q] = make_float2(x[su * inN + sv], 0.f);
+        constexpr int IB = WST_IN_BATCH;   // gather loads per thread in flight
+        for (int i0 = threadIdx.x; i0 < a.rows * n; i0 += IB * T) {
+            float xv[IB];
+#pragma unroll
+            for (int k = 0; k < IB; ++k) {
+                const int i = min(i0 + k * T, a.rows * n - 1);
+                const int rr = i / n, q = i - (i / n) * n;
+                const int u = r0 + rr;
+                const int su = p.pre_pad ? u : wstdev::reflect_index(u - p.padTop, p.M);
+                const int sv = p.pre_pad ? q : wstdev::reflect_index(q - p.padLeft, p.N);
+                xv[k] = x[su * inN + sv];
+            }
+#pragma unroll
+            for (int k = 0; k < IB; ++k) {
+                const int i = i0 + k * T;
+                const int rr = i / n, q = i - (i / n) * n;
+                if (i < a.rows * n) A[rr * ld + q] = make_float2(xv[k], 0.f);
+            }
         }
         __syncthreads();
         // S0 row partials T[p][c] = sum_q GN0[q][c] x[p][q] (natural order), 8 lanes per output
@@ -168,11 +218,51 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
         const float2* Cs = a.colt + static_cast<long long>(arr) * a.nrows * n;
         const int mm = 2 * (a.nrows - 1);
         const float mu = a.mean[arr];
-        for (int i = threadIdx.x; i < nlines * n; i += T) {
-            const int t = i / n, q = i - (i / n) * n;
-            float2 v = wstdev::ldnt(Cs + static_cast<long long>(r0 + t) * n + q);
-            if (r0 + t == 0) v.x += a.csum[static_cast<long long>(arr) * n + q] - static_cast<float>(mm) * mu;
-            A[t * ld + q] = v;
+        constexpr int IB = WST_IN_BATCH;   // loads per thread in flight
+        if constexpr (WST_WIDE_IO && N > 0 && N % 2 == 0) {
+            // element pairs per lane: 16-byte streaming loads
+            constexpr int H2 = N / 2;
+            for (int i0 = threadIdx.x; i0 < nlines * H2; i0 += IB * T) {
+                wst_f4 v[IB];
+#pragma unroll
+                for (int k = 0; k < IB; ++k) {
+                    const int i = min(i0 + k * T, nlines * H2 - 1);
+                    const int t = i / H2, q = 2 * (i - (i / H2) * H2);
+                    v[k] = ldnt2(Cs + static_cast<long long>(r0 + t) * n + q);
+                }
+#pragma unroll
+                for (int k = 0; k < IB; ++k) {
+                    const int i = i0 + k * T;
+                    const int t = i / H2, q = 2 * (i - (i / H2) * H2);
+                    if (i < nlines * H2) {
+                        float2 e0 = make_float2(v[k].x, v[k].y), e1 = make_float2(v[k].z, v[k].w);
+                        if (r0 + t == 0) {
+                            e0.x += a.csum[static_cast<long long>(arr) * n + q] - static_cast<float>(mm) * mu;
+                            e1.x += a.csum[static_cast<long long>(arr) * n + q + 1] - static_cast<float>(mm) * mu;
+                        }
+                        A[t * ld + q] = e0;
+                        A[t * ld + q + 1] = e1;
+                    }
+                }
+            }
+        } else
+        for (int i0 = threadIdx.x; i0 < nlines * n; i0 += IB * T) {
+            float2 v[IB];
+#pragma unroll
+            for (int k = 0; k < IB; ++k) {
+                const int i = min(i0 + k * T, nlines * n - 1);
+                const int t = i / n, q = i - (i / n) * n;
+                v[k] = wstdev::ldnt(Cs + static_cast<long long>(r0 + t) * n + q);
+            }
+#pragma unroll
+            for (int k = 0; k < IB; ++k) {
+                const int i = i0 + k * T;
+                const int t = i / n, q = i - (i / n) * n;
+                if (i < nlines * n) {
+                    if (r0 + t == 0) v[k].x += a.csum[static_cast<long long>(arr) * n + q] - static_cast<float>(mm) * mu;
+                    A[t * ld + q] = v[k];
+                }
+            }
         }
     } else if (a.mode == kRowFold1) {
         // arr = plane * L + l1: rows of fold_s(Xhat * psi0_{j1, l1}), Xhat is (m s) x (n s)
@@ -181,12 +271,39 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
         const int PN = n * s;
         const float2* X = a.xhat + static_cast<long long>(plane) * (m * s) * PN;
         const float* psi0 = p.psi + p.psi_off[(a.j1 * a.L + l1) * p.J + 0];
-        if (s == 1) {
-            for (int i0 = threadIdx.x; i0 < a.rows * n; i0 += kLoadBatch * T) {
-                float2 xv[kLoadBatch];
-                float f[kLoadBatch];
+        if (WST_WIDE_IO && N > 0 && N % 2 == 0 && s == 1) {
+            // element pairs per lane: Xhat as 16-byte loads (cacheable: every theta1 re-reads it),
+            // the real filter as 8-byte ones
+            constexpr int RB2 = ((N >= 384 && INV) ? WST_ROW_BATCH_384 : WST_ROW_BATCH) / 2;
+            constexpr int H2 = N > 0 ? N / 2 : 1;
+            for (int i0 = threadIdx.x; i0 < a.rows * H2; i0 += RB2 * T) {
+                wst_f4 xv[RB2];
+                float2 f[RB2];
 #pragma unroll
-                for (int k = 0; k < kLoadBatch; ++k) {
+                for (int k = 0; k < RB2; ++k) {
+                    const int i = min(i0 + k * T, a.rows * H2 - 1);
+                    const int rr = i / H2, q = 2 * (i - (i / H2) * H2);
+                    const long long idx = static_cast<long long>(r0 + rr) * PN + q;
+                    f[k] = *reinterpret_cast<const float2*>(psi0 + idx);
+                    xv[k] = *reinterpret_cast<const wst_f4*>(X + idx);
+                }
+#pragma unroll
+                for (int k = 0; k < RB2; ++k) {
+                    const int i = i0 + k * T;
+                    const int rr = i / H2, q = 2 * (i - (i / H2) * H2);
+                    if (i < a.rows * H2) {
+                        A[rr * ld + q] = make_float2(xv[k].x * f[k].x, xv[k].y * f[k].x);
+                        A[rr * ld + q + 1] = make_float2(xv[k].z * f[k].y, xv[k].w * f[k].y);
+                    }
+                }
+            }
+        } else if (s == 1) {
+            constexpr int RB = (N >= 384 && INV) ? WST_ROW_BATCH_384 : WST_ROW_BATCH;
+            for (int i0 = threadIdx.x; i0 < a.rows * n; i0 += RB * T) {
+                float2 xv[RB];
+                float f[RB];
+#pragma unroll
+                for (int k = 0; k < RB; ++k) {
                     const int i = min(i0 + k * T, a.rows * n - 1);
                     const int rr = i / n, q = i - (i / n) * n;
                     const long long idx = static_cast<long long>(r0 + rr) * PN + q;
@@ -194,10 +311,74 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
                     xv[k] = X[idx];
                 }
 #pragma unroll
-                for (int k = 0; k < kLoadBatch; ++k) {
+                for (int k = 0; k < RB; ++k) {
                     const int i = i0 + k * T;
                     const int rr = i / n, q = i - (i / n) * n;
                     if (i < a.rows * n) A[rr * ld + q] = make_float2(xv[k].x * f[k], xv[k].y * f[k]);
+                }
+            }
+        } else if (WST_WIDE_IO && N > 0 && N % 2 == 0 && s == 2) {
+            // the four aliases of element pairs: 16-byte Xhat loads, 8-byte filter loads
+            constexpr int IB2 = WST_IN_BATCH > 1 ? WST_IN_BATCH / 2 : 1;
+            constexpr int H2 = N > 0 ? N / 2 : 1;
+            for (int i0 = threadIdx.x; i0 < a.rows * H2; i0 += IB2 * T) {
+                wst_f4 xv[IB2][4];
+                float2 f[IB2][4];
+#pragma unroll
+                for (int k = 0; k < IB2; ++k) {
+                    const int i = min(i0 + k * T, a.rows * H2 - 1);
+                    const int rr = i / H2, q = 2 * (i - (i / H2) * H2);
+                    const int u = r0 + rr;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const long long idx = static_cast<long long>(u + (t >> 1) * m) * PN + q + (t & 1) * n;
+                        f[k][t] = *reinterpret_cast<const float2*>(psi0 + idx);
+                        xv[k][t] = *reinterpret_cast<const wst_f4*>(X + idx);
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < IB2; ++k) {
+                    const int i = i0 + k * T;
+                    const int rr = i / H2, q = 2 * (i - (i / H2) * H2);
+                    float2 acc0 = make_float2(0.f, 0.f), acc1 = make_float2(0.f, 0.f);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {   // same order as the generic loop (ii, jj)
+                        acc0 = make_float2(fmaf(xv[k][t].x, f[k][t].x, acc0.x), fmaf(xv[k][t].y, f[k][t].x, acc0.y));
+                        acc1 = make_float2(fmaf(xv[k][t].z, f[k][t].y, acc1.x), fmaf(xv[k][t].w, f[k][t].y, acc1.y));
+                    }
+                    if (i < a.rows * H2) {
+                        A[rr * ld + q] = acc0;
+                        A[rr * ld + q + 1] = acc1;
+                    }
+                }
+            }
+        } else if (WST_IN_BATCH > 1 && s == 2) {
+            // the four aliases of IB elements in flight (8 IB independent loads before the sums)
+            constexpr int IB = WST_IN_BATCH;
+            for (int i0 = threadIdx.x; i0 < a.rows * n; i0 += IB * T) {
+                float2 xv[IB][4];
+                float f[IB][4];
+#pragma unroll
+                for (int k = 0; k < IB; ++k) {
+                    const int i = min(i0 + k * T, a.rows * n - 1);
+                    const int rr = i / n, q = i - (i / n) * n;
+                    const int u = r0 + rr;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const long long idx = static_cast<long long>(u + (t >> 1) * m) * PN + q + (t & 1) * n;
+                        f[k][t] = psi0[idx];
+                        xv[k][t] = X[idx];
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < IB; ++k) {
+                    const int i = i0 + k * T;
+                    const int rr = i / n, q = i - (i / n) * n;
+                    float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)   // same order as the generic loop (ii, jj)
+                        acc = make_float2(fmaf(xv[k][t].x, f[k][t], acc.x), fmaf(xv[k][t].y, f[k][t], acc.y));
+                    if (i < a.rows * n) A[rr * ld + q] = acc;
                 }
             }
         } else
@@ -245,13 +426,67 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
                         fo[k][t] = kr * n1 + kc;
                     }
                 }
-                for (int pr = 0; pr < a.npair; ++pr) {
-                    const float2* ps = a.psi2 + pr * a.pstride;
-                    float2 f[KI][4];
+                float2 fn[KI][4];   // WST_FOLD_PREFETCH: the next pair's taps, loaded one pair ahead
+                if constexpr (WST_FOLD_PREFETCH) {
 #pragma unroll
                     for (int k = 0; k < KI; ++k)
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) f[k][t] = ps[fo[k][t]];
+                        for (int t = 0; t < 4; ++t) fn[k][t] = a.psi2[fo[k][t]];
+                }
+                if constexpr (WST_FOLD_PG > 1) {
+                    // WST_FOLD_PG pairs' taps in flight together (their loads issued before any sum)
+                    constexpr int PG = WST_FOLD_PG;
+                    for (int pr0 = 0; pr0 < a.npair; pr0 += PG) {
+                        float2 f[PG][KI][4];
+#pragma unroll
+                        for (int g = 0; g < PG; ++g) {
+                            const float2* ps = a.psi2 + min(pr0 + g, a.npair - 1) * a.pstride;
+#pragma unroll
+                            for (int k = 0; k < KI; ++k)
+#pragma unroll
+                                for (int t = 0; t < 4; ++t) f[g][k][t] = ps[fo[k][t]];
+                        }
+#pragma unroll
+                        for (int g = 0; g < PG; ++g) {
+                            const int pr = pr0 + g;
+                            if (pr >= a.npair) break;
+#pragma unroll
+                            for (int k = 0; k < KI; ++k) {
+                                const int i = i0 + k * T;
+                                if (i >= a.rows * n) break;
+                                const int rr = i / n, v = i - (i / n) * n;
+                                float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+#pragma unroll
+                                for (int t = 0; t < 4; ++t) {
+                                    a0 = make_float2(fmaf(h[k][t].x, f[g][k][t].x, a0.x), fmaf(h[k][t].y, f[g][k][t].x, a0.y));
+                                    a1 = make_float2(fmaf(h[k][t].x, f[g][k][t].y, a1.x), fmaf(h[k][t].y, f[g][k][t].y, a1.y));
+                                }
+                                A[(2 * pr * a.rows + rr) * ld + v] = a0;
+                                if (2 * pr + 1 < a.npath) A[((2 * pr + 1) * a.rows + rr) * ld + v] = a1;
+                            }
+                        }
+                    }
+                    continue;
+                }
+                for (int pr = 0; pr < a.npair; ++pr) {
+                    const float2* ps = a.psi2 + pr * a.pstride;
+                    float2 f[KI][4];
+                    if constexpr (WST_FOLD_PREFETCH) {
+                        (void)ps;
+                        const float2* pn = a.psi2 + min(pr + 1, a.npair - 1) * a.pstride;
+#pragma unroll
+                        for (int k = 0; k < KI; ++k)
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) {
+                                f[k][t] = fn[k][t];
+                                fn[k][t] = pn[fo[k][t]];
+                            }
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < KI; ++k)
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) f[k][t] = ps[fo[k][t]];
+                    }
 #pragma unroll
                     for (int k = 0; k < KI; ++k) {
                         const int i = i0 + k * T;
@@ -270,6 +505,17 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
             }
             __syncthreads();
             big_fft<N, INV>(A, wstfft::Lines(1, 0, a.npath * a.rows, ld, 1), n, tw, id);
+            if constexpr (WST_WIDE_IO && N > 0 && N % 2 == 0) {
+                // element pairs (q, q + 1) per lane: 16-byte streaming stores
+                constexpr int H2 = N / 2;
+                for (int i = threadIdx.x; i < a.npath * a.rows * H2; i += T) {
+                    const int line = i / H2, q = 2 * (i - (i / H2) * H2);
+                    const int path = line / a.rows, rr = line - path * a.rows;
+                    float2* D = a.dst + (static_cast<long long>(arr) * a.npath + path) * m * n;
+                    stnt2(D + (r0 + rr) * n + q, A[line * ld + q], A[line * ld + q + 1]);
+                }
+                return;
+            }
             for (int i = threadIdx.x; i < a.npath * a.rows * n; i += T) {
                 const int line = i / n, q = i - (i / n) * n;
                 const int path = line / a.rows, rr = line - path * a.rows;
@@ -343,6 +589,14 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
     }
     if (a.mode == kRowPad || a.mode == kRowFold1) {
         float2* D = a.dst + static_cast<long long>(arr) * m * n;
+        if constexpr (WST_WIDE_IO && N > 0 && N % 2 == 0) {
+            constexpr int H2 = N / 2;   // element pairs per lane: 16-byte streaming stores
+            for (int i = threadIdx.x; i < a.rows * H2; i += T) {
+                const int rr = i / H2, q = 2 * (i - (i / H2) * H2);
+                stnt2(D + (r0 + rr) * n + q, A[rr * ld + q], A[rr * ld + q + 1]);
+            }
+            return;
+        }
         for (int i = threadIdx.x; i < a.rows * n; i += T) {
             const int rr = i / n, q = i - (i / n) * n;
             wstdev::stnt(D + (r0 + rr) * n + q, A[rr * ld + q]);
@@ -373,6 +627,19 @@ __device__ __forceinline__ void col_spectra(float2* A, const float2* tw, const B
     big_fft<N, false>(A, wstfft::Lines(1, 0, npair, 2 * ld, 1), n, tw, id);
     const int hrows = n / 2 + 1;
     float2* D = a.colt + static_cast<long long>(arr) * hrows * a.ncols;
+    if constexpr (WST_WIDE_IO && N > 0) if ((nc & 1) == 0 && (a.ncols & 1) == 0) {
+        // both columns of a packed pair from one lane: one 16-byte streaming store
+        for (int i = threadIdx.x; i < hrows * (kColTile / 2); i += T) {
+            const int k1 = i / (kColTile / 2), cp = i - (i / (kColTile / 2)) * (kColTile / 2);
+            if (2 * cp >= nc) continue;
+            const float2 z = A[2 * cp * ld + k1];
+            const float2 zm = A[2 * cp * ld + (k1 == 0 ? 0 : n - k1)];
+            stnt2(D + static_cast<long long>(k1) * a.ncols + c0 + 2 * cp,
+                  make_float2(0.5f * (z.x + zm.x), 0.5f * (z.y - zm.y)),
+                  make_float2(0.5f * (z.y + zm.y), -0.5f * (z.x - zm.x)));
+        }
+        return;
+    }
     for (int i = threadIdx.x; i < hrows * kColTile; i += T) {
         const int k1 = i / kColTile, c = i - (i / kColTile) * kColTile;
         if (c >= nc) continue;
@@ -411,16 +678,44 @@ __global__ void __launch_bounds__(big_col_threads(N)) k_big_cols(DevParams p, Bi
     float2* src = a.dst + static_cast<long long>(arr) * n * a.ncols;
     // kLoadBatch loads per thread in flight before their LDS stores (a load-store loop waits out
     // the HBM latency once per element: ~2.2 TB/s at c5)
-    for (int i0 = threadIdx.x; i0 < n * C; i0 += kLoadBatch * T) {
-        float2 t[kLoadBatch];
+    constexpr int TB = col_tile_batch(N);
+    bool wide_done = false;
+    if constexpr (WST_WIDE_IO && N > 0) if ((nc & 1) == 0 && (a.ncols & 1) == 0) {
+        // column pairs (2c, 2c + 1) of a row per lane: 16-byte streaming loads, 8 lanes per 128 B
+        wide_done = true;
+        constexpr int C2 = C / 2;
+        constexpr int TB2 = (N * C2 + big_col_threads(N) - 1) / big_col_threads(N);
+        const int nc2 = nc / 2;
+        for (int i0 = threadIdx.x; i0 < n * C2; i0 += TB2 * T) {
+            wst_f4 t[TB2];
 #pragma unroll
-        for (int k = 0; k < kLoadBatch; ++k) {
+            for (int k = 0; k < TB2; ++k) {
+                const int i = min(i0 + k * T, n * C2 - 1);
+                const int u = i / C2, c = min(i - (i / C2) * C2, nc2 - 1);
+                t[k] = ldnt2(src + static_cast<long long>(u) * a.ncols + c0 + 2 * c);
+            }
+#pragma unroll
+            for (int k = 0; k < TB2; ++k) {
+                const int i = i0 + k * T;
+                const int u = i / C2, c = i - (i / C2) * C2;
+                if (i < n * C2 && c < nc2) {
+                    A[(2 * c) * ld + u] = make_float2(t[k].x, t[k].y);
+                    A[(2 * c + 1) * ld + u] = make_float2(t[k].z, t[k].w);
+                }
+            }
+        }
+    }
+    if (!wide_done)
+    for (int i0 = threadIdx.x; i0 < n * C; i0 += TB * T) {
+        float2 t[TB];
+#pragma unroll
+        for (int k = 0; k < TB; ++k) {
             const int i = min(i0 + k * T, n * C - 1);
             const int u = i / C, c = min(i - (i / C) * C, nc - 1);
             t[k] = wstdev::ldnt(src + static_cast<long long>(u) * a.ncols + c0 + c);
         }
 #pragma unroll
-        for (int k = 0; k < kLoadBatch; ++k) {
+        for (int k = 0; k < TB; ++k) {
             const int i = i0 + k * T;
             const int u = i / C, c = i - (i / C) * C;
             if (i < n * C && c < nc) A[c * ld + u] = t[k];
@@ -430,6 +725,13 @@ __global__ void __launch_bounds__(big_col_threads(N)) k_big_cols(DevParams p, Bi
     if (a.mode == kColStore) {
         wstfft::EpiIdentity id;
         big_fft<N, INV>(A, wstfft::Lines(1, 0, nc, ld, 1), n, tw, id);
+        if (wide_done) {   // column pairs per lane: 16-byte streaming stores
+            for (int i = threadIdx.x; i < n * (C / 2); i += T) {
+                const int u = i / (C / 2), c = 2 * (i - (i / (C / 2)) * (C / 2));
+                if (c < nc) stnt2(src + static_cast<long long>(u) * a.ncols + c0 + c, A[c * ld + u], A[(c + 1) * ld + u]);
+            }
+            return;
+        }
         for (int i = threadIdx.x; i < n * C; i += T) {
             const int u = i / C, c = i - (i / C) * C;
             if (c < nc) wstdev::stnt(src + static_cast<long long>(u) * a.ncols + c0 + c, A[c * ld + u]);
