@@ -39,27 +39,25 @@ constexpr int big_col_threads(int n) { return n >= 384 ? 512 : 256; }
 constexpr int kColTile = 16;         // columns per column-pass workgroup (128 B rows)
 constexpr int kMeanParts = 16;                  // k_big_mean partial sums per plane
 constexpr int kLoadBatch = 8;                   // global loads per thread in flight (tile loads)
-#ifndef WST_TILE_BATCH_MAX   // A/B builds: column-tile loads per thread in flight (compiled lengths)
-#define WST_TILE_BATCH_MAX 16
-#endif
-#ifndef WST_ROW_BATCH        // A/B builds: kRowFold1 (s = 1) loads per thread in flight
-#define WST_ROW_BATCH 8
-#endif
-#ifndef WST_FOLD_PREFETCH    // A/B builds: fold_all loads the next pair's filter taps one pair ahead
-#define WST_FOLD_PREFETCH 0
-#endif
-#ifndef WST_ROW_BATCH_384    // A/B builds: kRowFold1 (s = 1) loads in flight at the 384-point level
-#define WST_ROW_BATCH_384 WST_ROW_BATCH
-#endif
-#ifndef WST_IN_BATCH         // A/B builds: kRowPad / kRowHalf / kRowFold1 (s = 2) loads in flight
-#define WST_IN_BATCH 1
-#endif
-#ifndef WST_FOLD_PG          // A/B builds: fold_all filter pairs whose taps are loaded together
-#define WST_FOLD_PG 1
-#endif
-#ifndef WST_WIDE_IO          // A/B builds: 16-byte (two-element) column-tile loads / fold_all stores
-#define WST_WIDE_IO 0
-#endif
+// Loads per thread in flight in the staged passes (measured at c5, profiles/r06_ab.txt r06n-r06q):
+// a compiled length's whole column-tile share in one batch (12 at 192 and 384 points: -2 %), the
+// 384-point s = 1 order-1 row fold 24 per batch, the reflect-pad gather / column-spectrum rows /
+// s = 2 order-1 row fold kInBatch per batch (each was one load per loop iteration: -5 %)
+constexpr int kTileBatchMax = 16;
+constexpr int kRowBatch = 8;
+constexpr int kRowBatch384 = 24;
+constexpr int kInBatch = 4;
+// Column-tile loads per thread in flight: a compiled length's whole tile share (N x kColTile /
+// threads) in one batch, up to kTileBatchMax; runtime lengths kLoadBatch
+constexpr int col_tile_batch(int N) {
+    return N > 0 ? ((N * kColTile + big_col_threads(N) - 1) / big_col_threads(N) < kTileBatchMax
+                        ? (N * kColTile + big_col_threads(N) - 1) / big_col_threads(N)
+                        : kTileBatchMax)
+                 : kLoadBatch;
+}
+// 16-byte streaming I/O: compiled (even) lengths move element pairs per lane -- column-tile loads,
+// row-pass and column-spectrum stores, the column-spectrum rows' loads, Xhat in the order-1 row
+// folds (8-byte accesses stream at a fraction of the 16-byte rate; c5 -4 %, r06p / r06q)
 typedef float wst_f4 __attribute__((ext_vector_type(4)));
 // two consecutive complex elements as one 16-byte streaming load / store (16-byte aligned)
 __device__ __forceinline__ wst_f4 ldnt2(const float2* p) {
@@ -68,14 +66,6 @@ __device__ __forceinline__ wst_f4 ldnt2(const float2* p) {
 __device__ __forceinline__ void stnt2(float2* p, float2 a, float2 b) {
     wst_f4 v = {a.x, a.y, b.x, b.y};
     __builtin_nontemporal_store(v, reinterpret_cast<wst_f4*>(p));
-}
-// Column-tile loads per thread in flight: a compiled length's whole tile share (N x kColTile /
-// threads: 12 at 192 and 384) in one batch, up to WST_TILE_BATCH_MAX; runtime lengths kLoadBatch
-constexpr int col_tile_batch(int N) {
-    return N > 0 ? ((N * kColTile + big_col_threads(N) - 1) / big_col_threads(N) < WST_TILE_BATCH_MAX
-                        ? (N * kColTile + big_col_threads(N) - 1) / big_col_threads(N)
-                        : WST_TILE_BATCH_MAX)
-                 : kLoadBatch;
 }
 constexpr int kBigOGroup = 16;                  // outputs per accumulation round of wide low-passes
 
@@ -172,7 +162,7 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
         // arr = chunk-local plane; raw values first (S0 partials), then mean-centred
         const int inM = p.pre_pad ? p.PM : p.M, inN = p.pre_pad ? p.PN : p.N;
         const float* x = a.in + static_cast<long long>(arr) * inM * inN;
-        constexpr int IB = WST_IN_BATCH;   // gather loads per thread in flight
+        constexpr int IB = kInBatch;   // gather loads per thread in flight
         for (int i0 = threadIdx.x; i0 < a.rows * n; i0 += IB * T) {
             float xv[IB];
 #pragma unroll
@@ -218,8 +208,8 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
         const float2* Cs = a.colt + static_cast<long long>(arr) * a.nrows * n;
         const int mm = 2 * (a.nrows - 1);
         const float mu = a.mean[arr];
-        constexpr int IB = WST_IN_BATCH;   // loads per thread in flight
-        if constexpr (WST_WIDE_IO && N > 0 && N % 2 == 0) {
+        constexpr int IB = kInBatch;   // loads per thread in flight
+        if constexpr (N > 0 && N % 2 == 0) {
             // element pairs per lane: 16-byte streaming loads
             constexpr int H2 = N / 2;
             for (int i0 = threadIdx.x; i0 < nlines * H2; i0 += IB * T) {
@@ -271,10 +261,10 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
         const int PN = n * s;
         const float2* X = a.xhat + static_cast<long long>(plane) * (m * s) * PN;
         const float* psi0 = p.psi + p.psi_off[(a.j1 * a.L + l1) * p.J + 0];
-        if (WST_WIDE_IO && N > 0 && N % 2 == 0 && s == 1) {
+        if (N > 0 && N % 2 == 0 && s == 1) {
             // element pairs per lane: Xhat as 16-byte loads (cacheable: every theta1 re-reads it),
             // the real filter as 8-byte ones
-            constexpr int RB2 = ((N >= 384 && INV) ? WST_ROW_BATCH_384 : WST_ROW_BATCH) / 2;
+            constexpr int RB2 = ((N >= 384 && INV) ? kRowBatch384 : kRowBatch) / 2;
             constexpr int H2 = N > 0 ? N / 2 : 1;
             for (int i0 = threadIdx.x; i0 < a.rows * H2; i0 += RB2 * T) {
                 wst_f4 xv[RB2];
@@ -298,7 +288,7 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
                 }
             }
         } else if (s == 1) {
-            constexpr int RB = (N >= 384 && INV) ? WST_ROW_BATCH_384 : WST_ROW_BATCH;
+            constexpr int RB = (N >= 384 && INV) ? kRowBatch384 : kRowBatch;
             for (int i0 = threadIdx.x; i0 < a.rows * n; i0 += RB * T) {
                 float2 xv[RB];
                 float f[RB];
@@ -317,9 +307,9 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
                     if (i < a.rows * n) A[rr * ld + q] = make_float2(xv[k].x * f[k], xv[k].y * f[k]);
                 }
             }
-        } else if (WST_WIDE_IO && N > 0 && N % 2 == 0 && s == 2) {
+        } else if (N > 0 && N % 2 == 0 && s == 2) {
             // the four aliases of element pairs: 16-byte Xhat loads, 8-byte filter loads
-            constexpr int IB2 = WST_IN_BATCH > 1 ? WST_IN_BATCH / 2 : 1;
+            constexpr int IB2 = kInBatch > 1 ? kInBatch / 2 : 1;
             constexpr int H2 = N > 0 ? N / 2 : 1;
             for (int i0 = threadIdx.x; i0 < a.rows * H2; i0 += IB2 * T) {
                 wst_f4 xv[IB2][4];
@@ -352,9 +342,9 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
                     }
                 }
             }
-        } else if (WST_IN_BATCH > 1 && s == 2) {
+        } else if (kInBatch > 1 && s == 2) {
             // the four aliases of IB elements in flight (8 IB independent loads before the sums)
-            constexpr int IB = WST_IN_BATCH;
+            constexpr int IB = kInBatch;
             for (int i0 = threadIdx.x; i0 < a.rows * n; i0 += IB * T) {
                 float2 xv[IB][4];
                 float f[IB][4];
@@ -426,67 +416,13 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
                         fo[k][t] = kr * n1 + kc;
                     }
                 }
-                float2 fn[KI][4];   // WST_FOLD_PREFETCH: the next pair's taps, loaded one pair ahead
-                if constexpr (WST_FOLD_PREFETCH) {
-#pragma unroll
-                    for (int k = 0; k < KI; ++k)
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) fn[k][t] = a.psi2[fo[k][t]];
-                }
-                if constexpr (WST_FOLD_PG > 1) {
-                    // WST_FOLD_PG pairs' taps in flight together (their loads issued before any sum)
-                    constexpr int PG = WST_FOLD_PG;
-                    for (int pr0 = 0; pr0 < a.npair; pr0 += PG) {
-                        float2 f[PG][KI][4];
-#pragma unroll
-                        for (int g = 0; g < PG; ++g) {
-                            const float2* ps = a.psi2 + min(pr0 + g, a.npair - 1) * a.pstride;
-#pragma unroll
-                            for (int k = 0; k < KI; ++k)
-#pragma unroll
-                                for (int t = 0; t < 4; ++t) f[g][k][t] = ps[fo[k][t]];
-                        }
-#pragma unroll
-                        for (int g = 0; g < PG; ++g) {
-                            const int pr = pr0 + g;
-                            if (pr >= a.npair) break;
-#pragma unroll
-                            for (int k = 0; k < KI; ++k) {
-                                const int i = i0 + k * T;
-                                if (i >= a.rows * n) break;
-                                const int rr = i / n, v = i - (i / n) * n;
-                                float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
-#pragma unroll
-                                for (int t = 0; t < 4; ++t) {
-                                    a0 = make_float2(fmaf(h[k][t].x, f[g][k][t].x, a0.x), fmaf(h[k][t].y, f[g][k][t].x, a0.y));
-                                    a1 = make_float2(fmaf(h[k][t].x, f[g][k][t].y, a1.x), fmaf(h[k][t].y, f[g][k][t].y, a1.y));
-                                }
-                                A[(2 * pr * a.rows + rr) * ld + v] = a0;
-                                if (2 * pr + 1 < a.npath) A[((2 * pr + 1) * a.rows + rr) * ld + v] = a1;
-                            }
-                        }
-                    }
-                    continue;
-                }
                 for (int pr = 0; pr < a.npair; ++pr) {
                     const float2* ps = a.psi2 + pr * a.pstride;
                     float2 f[KI][4];
-                    if constexpr (WST_FOLD_PREFETCH) {
-                        (void)ps;
-                        const float2* pn = a.psi2 + min(pr + 1, a.npair - 1) * a.pstride;
 #pragma unroll
-                        for (int k = 0; k < KI; ++k)
+                    for (int k = 0; k < KI; ++k)
 #pragma unroll
-                            for (int t = 0; t < 4; ++t) {
-                                f[k][t] = fn[k][t];
-                                fn[k][t] = pn[fo[k][t]];
-                            }
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < KI; ++k)
-#pragma unroll
-                            for (int t = 0; t < 4; ++t) f[k][t] = ps[fo[k][t]];
-                    }
+                        for (int t = 0; t < 4; ++t) f[k][t] = ps[fo[k][t]];
 #pragma unroll
                     for (int k = 0; k < KI; ++k) {
                         const int i = i0 + k * T;
@@ -505,7 +441,7 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
             }
             __syncthreads();
             big_fft<N, INV>(A, wstfft::Lines(1, 0, a.npath * a.rows, ld, 1), n, tw, id);
-            if constexpr (WST_WIDE_IO && N > 0 && N % 2 == 0) {
+            if constexpr (N > 0 && N % 2 == 0) {
                 // element pairs (q, q + 1) per lane: 16-byte streaming stores
                 constexpr int H2 = N / 2;
                 for (int i = threadIdx.x; i < a.npath * a.rows * H2; i += T) {
@@ -589,7 +525,7 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
     }
     if (a.mode == kRowPad || a.mode == kRowFold1) {
         float2* D = a.dst + static_cast<long long>(arr) * m * n;
-        if constexpr (WST_WIDE_IO && N > 0 && N % 2 == 0) {
+        if constexpr (N > 0 && N % 2 == 0) {
             constexpr int H2 = N / 2;   // element pairs per lane: 16-byte streaming stores
             for (int i = threadIdx.x; i < a.rows * H2; i += T) {
                 const int rr = i / H2, q = 2 * (i - (i / H2) * H2);
@@ -627,7 +563,7 @@ __device__ __forceinline__ void col_spectra(float2* A, const float2* tw, const B
     big_fft<N, false>(A, wstfft::Lines(1, 0, npair, 2 * ld, 1), n, tw, id);
     const int hrows = n / 2 + 1;
     float2* D = a.colt + static_cast<long long>(arr) * hrows * a.ncols;
-    if constexpr (WST_WIDE_IO && N > 0) if ((nc & 1) == 0 && (a.ncols & 1) == 0) {
+    if constexpr (N > 0) if ((nc & 1) == 0 && (a.ncols & 1) == 0) {
         // both columns of a packed pair from one lane: one 16-byte streaming store
         for (int i = threadIdx.x; i < hrows * (kColTile / 2); i += T) {
             const int k1 = i / (kColTile / 2), cp = i - (i / (kColTile / 2)) * (kColTile / 2);
@@ -680,7 +616,7 @@ __global__ void __launch_bounds__(big_col_threads(N)) k_big_cols(DevParams p, Bi
     // the HBM latency once per element: ~2.2 TB/s at c5)
     constexpr int TB = col_tile_batch(N);
     bool wide_done = false;
-    if constexpr (WST_WIDE_IO && N > 0) if ((nc & 1) == 0 && (a.ncols & 1) == 0) {
+    if constexpr (N > 0) if ((nc & 1) == 0 && (a.ncols & 1) == 0) {
         // column pairs (2c, 2c + 1) of a row per lane: 16-byte streaming loads, 8 lanes per 128 B
         wide_done = true;
         constexpr int C2 = C / 2;
