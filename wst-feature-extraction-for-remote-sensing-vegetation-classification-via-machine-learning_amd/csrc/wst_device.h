@@ -64,9 +64,6 @@ constexpr int fused_row_n2(int n) { return n == 48 ? 8 : 0; }
 #endif
 constexpr int fused_col_n2(int n) { return n == 48 ? WST_COL48_N2 : 0; }
 constexpr int kPrepBatch = 8;   // k_prep gather loads per thread in flight
-#ifndef WST_BOX_BB   // A/B builds: bins per lane in the HG kernels' box folds
-#define WST_BOX_BB 1
-#endif
 #ifndef WST_O1_PACK_HALF   // A/B builds (tools/variant.sh -DWST_O1_PACK_HALF=0: k_o1 packs rows 2r, 2r + 1)
 #define WST_O1_PACK_HALF 1
 #endif
@@ -1427,7 +1424,7 @@ __device__ __forceinline__ float2 buf_load2(__amdgpu_buffer_rsrc_t r, int voff, 
 // Column taps go in blocks of four, set up once per block (H column, mirror, sign; taps past the
 // box are skipped), then the block walks the box rows: per tap one read of H, one buffer load
 // (32-bit offsets) and the products.
-template <int S, int BB = 1>
+template <int S>
 __device__ __forceinline__ void fold2(const float2* __restrict__ H, int hld, int nM1, int nN1,
                                       const float2* __restrict__ psi2, long long pstride,
                                       int npair, int npath, float2* __restrict__ B, int pslot,
@@ -1440,93 +1437,6 @@ __device__ __forceinline__ void fold2(const float2* __restrict__ H, int hld, int
     const int total = npair * items;
     const wstfft::FastDiv ditems(items), dn(nN2);
     const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, static_cast<int>(npair * pstride * 8));
-    if constexpr (BB > 1) {
-        // BB bins per lane: their box headers, then for every (column block, row) of the larger box
-        // the taps of every bin at once, so BB bins' HBM / L2 loads are in flight together (c5's
-        // HG folds read the staged spectrum: one bin per lane waited out its latency per box row)
-        const int T = blockDim.x;
-        for (int w0 = threadIdx.x; w0 < total; w0 += BB * T) {
-            int u[BB], v[BB], i0[BB], ni[BB], j0[BB], nj[BB], fpr[BB], pr[BB];
-#pragma unroll
-            for (int b = 0; b < BB; ++b) {
-                const int w = w0 + b * T;
-                const int wc = min(w, total - 1);
-                pr[b] = ditems.div(wc);
-                const int it = wc - pr[b] * items;
-                u[b] = dn.div(it);
-                v[b] = it - u[b] * nN2;
-                const int* bx = box + pr[b] * bstride;
-                const int rb = bx[u[b]], cb = bx[nM2 + v[b]];
-                i0[b] = rb & 255;
-                ni[b] = w < total ? rb >> 8 : 0;
-                j0[b] = cb & 255;
-                nj[b] = w < total ? cb >> 8 : 0;
-                fpr[b] = static_cast<int>(pr[b] * pstride);
-            }
-            int nim = ni[0], njm = nj[0];
-#pragma unroll
-            for (int b = 1; b < BB; ++b) {
-                nim = max(nim, ni[b]);
-                njm = max(njm, nj[b]);
-            }
-            float2 a0[BB], a1[BB];
-#pragma unroll
-            for (int b = 0; b < BB; ++b) a0[b] = a1[b] = make_float2(0.f, 0.f);
-            for (int jb = 0; jb < njm; jb += 4) {
-                int hc[BB][4], fc[BB][4];
-                bool mir[BB][4], ok[BB][4];
-                float wy[BB][4];
-#pragma unroll
-                for (int b = 0; b < BB; ++b)
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        ok[b][c] = jb + c < nj[b];
-                        const int kc = v[b] + ((j0[b] + jb + c) & smask) * nN2;
-                        mir[b][c] = kc > half;
-                        hc[b][c] = mir[b][c] ? nN1 - kc : kc;
-                        fc[b][c] = kc * 8;
-                        wy[b][c] = mir[b][c] ? -1.f : 1.f;
-                    }
-                for (int i = 0; i < nim; ++i) {
-                    float2 hv[BB][4], fv[BB][4];
-#pragma unroll
-                    for (int b = 0; b < BB; ++b) {
-                        const int kr = u[b] + ((i0[b] + i) & smask) * nM2;
-                        const int krm = kr == 0 ? 0 : nM1 - kr;
-                        const float2* hd = H + kr * hld;
-                        const float2* hm = H + krm * hld;
-                        const int fo = (fpr[b] + kr * nN1) * 8;
-                        const bool row = i < ni[b];
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            hv[b][c] = make_float2(0.f, 0.f);
-                            fv[b][c] = make_float2(0.f, 0.f);
-                            if (row && ok[b][c]) {
-                                hv[b][c] = (mir[b][c] ? hm : hd)[hc[b][c]];
-                                fv[b][c] = buf_load2(rs, fo + fc[b][c], 0);
-                            }
-                        }
-                    }
-#pragma unroll
-                    for (int b = 0; b < BB; ++b)
-#pragma unroll
-                        for (int c = 0; c < 4; ++c) {
-                            const float hx = hv[b][c].x, hy = hv[b][c].y * wy[b][c];
-                            a0[b] = make_float2(fmaf(hx, fv[b][c].x, a0[b].x), fmaf(hy, fv[b][c].x, a0[b].y));
-                            a1[b] = make_float2(fmaf(hx, fv[b][c].y, a1[b].x), fmaf(hy, fv[b][c].y, a1[b].y));
-                        }
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < BB; ++b) {
-                if (w0 + b * T >= total) break;
-                float2* dst = B + 2 * pr[b] * pslot + u[b] * ld2 + v[b];
-                dst[0] = a0[b];
-                if (2 * pr[b] + 1 < npath) dst[pslot] = a1[b];
-            }
-        }
-        return;
-    }
     for (int w = threadIdx.x; w < total; w += blockDim.x) {
         const int pr = ditems.div(w);
         const int it = w - pr * items;
@@ -1652,7 +1562,7 @@ __device__ __forceinline__ void fold2_any(int s2, const float2* H, int hld, int 
                                           int npath, float2* B, int pslot, int ld2, int nM2,
                                           int nN2, const int* box, int bstride) {
     if (s2 == 2) fold2_s2<R>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
-    else fold2<0, R == 2 ? WST_BOX_BB : 1>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, s2, box, bstride);
+    else fold2<0>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, s2, box, bstride);
 }
 
 // ---- tile-mapped folds of a square level with compile-time sizes (SQ geometry kernels) ----
