@@ -1556,12 +1556,101 @@ __device__ __forceinline__ void fold2_s2(const float2* __restrict__ H, int hld, 
     }
 }
 
+// Two adjacent columns (v, v + 1) per lane (even nN2): the filter taps of both as one 16-byte
+// buffer load (offsets (pr pstride + u nN1 + v) even), the spectrum taps 8-byte (the mirror runs
+// backwards over odd-length rows); rows walked in steps of T / (nN2 / 2).
+__device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+template <int R = 1>
+__device__ __forceinline__ void fold2_s2_pairs(const float2* __restrict__ H, int hld, int nM1, int nN1,
+                                               const float2* __restrict__ psi2, long long pstride,
+                                               int npair, int npath, float2* __restrict__ B, int pslot,
+                                               int ld2, int nM2, int nN2) {
+    const int nh = nN2 >> 1;
+    const int rpp = blockDim.x / nh;
+    const int t0 = threadIdx.x / nh;
+    if (t0 >= rpp) return;
+    const int v = 2 * (threadIdx.x - t0 * nh);
+    const int hq = nM2 * hld;
+    const int fq = nM2 * nN1 * 8;
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, static_cast<int>(npair * pstride * 8));
+    const wstfft::FastDiv dm(nM2);
+    const int rows = npair * nM2;
+    for (int pu0 = t0; pu0 < rows; pu0 += R * rpp) {
+        float2 h[R][2][4];
+        float4 f[R][4];
+        int pr[R], dst[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int pu = min(pu0 + r * rpp, rows - 1);
+            pr[r] = dm.div(pu);
+            const int u = pu - pr[r] * nM2;
+            dst[r] = pu0 + r * rpp < rows ? 2 * pr[r] * pslot + u * ld2 + v : -1;
+            const int hr = u * hld;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int c = v + e;
+                const bool c0 = c == 0;
+                const int cB = c0 ? nN2 : nN2 - c;
+                const int hm0 = c0 ? hr : (u == 0 ? 0 : (nM1 - u) * hld);
+                const int hm1 = c0 ? hr + hq : (nM2 - u) * hld;
+                h[r][e][0] = H[hr + c];
+                h[r][e][1] = H[hm0 + cB];
+                h[r][e][2] = H[hr + hq + c];
+                h[r][e][3] = H[hm1 + cB];
+                const float sg = c0 ? 1.f : -1.f;
+                h[r][e][1].y *= sg;
+                h[r][e][3].y *= sg;
+            }
+            const int fo = (static_cast<int>(pr[r] * pstride) + u * nN1 + v) * 8;
+            f[r][0] = buf_load4(rs, fo, 0);
+            f[r][1] = buf_load4(rs, fo, nN2 * 8);
+            f[r][2] = buf_load4(rs, fo, fq);
+            f[r][3] = buf_load4(rs, fo, fq + nN2 * 8);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                float fa[4], fb[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    fa[t] = e ? f[r][t].z : f[r][t].x;
+                    fb[t] = e ? f[r][t].w : f[r][t].y;
+                }
+                const float2* hh = h[r][e];
+                float2 a0, a1;
+                a0.x = fmaf(hh[0].x, fa[0], fmaf(hh[1].x, fa[1], fmaf(hh[2].x, fa[2], hh[3].x * fa[3])));
+                a0.y = fmaf(hh[0].y, fa[0], fmaf(hh[1].y, fa[1], fmaf(hh[2].y, fa[2], hh[3].y * fa[3])));
+                a1.x = fmaf(hh[0].x, fb[0], fmaf(hh[1].x, fb[1], fmaf(hh[2].x, fb[2], hh[3].x * fb[3])));
+                a1.y = fmaf(hh[0].y, fb[0], fmaf(hh[1].y, fb[1], fmaf(hh[2].y, fb[2], hh[3].y * fb[3])));
+                if (dst[r] >= 0) {
+                    float2* d = B + dst[r] + e;
+                    d[0] = a0;
+                    if (2 * pr[r] + 1 < npath) d[pslot] = a1;
+                }
+            }
+        }
+    }
+}
+
 template <int R = 1>
 __device__ __forceinline__ void fold2_any(int s2, const float2* H, int hld, int nM1, int nN1,
                                           const float2* psi2, long long pstride, int npair,
                                           int npath, float2* B, int pslot, int ld2, int nM2,
                                           int nN2, const int* box, int bstride) {
-    if (s2 == 2) fold2_s2<R>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
+    if (s2 == 2) {
+        // column pairs where they keep > 6 % more lanes busy (f3's 68-column paths on 512 lanes:
+        // 476 -> 510, k_o2 1.216 -> 1.166 ms; c1's 36 columns on 256 lanes gain no lanes and
+        // measured 1.3 % slower, c5's 96 on 1024 +5 % lanes, neutral; profiles/r06_ab.txt r06w),
+        // one row pair per lane in flight (two: 0.6 % slower, three: 4 %; r06x)
+        const int T = blockDim.x;
+        if (R == 2 && (nN2 & 1) == 0 && (T / (nN2 >> 1)) * (nN2 >> 1) * 100 > (T / nN2) * nN2 * 106)
+            fold2_s2_pairs<1>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
+        else
+            fold2_s2<R>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
+    }
     else fold2<0>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2, s2, box, bstride);
 }
 

@@ -398,6 +398,50 @@ __global__ void __launch_bounds__(kBigThreads) k_big_rows(DevParams p, BigArgs a
             // bytes at c5); path p of row rr lands on line p * rows + rr
             // KI bins per thread in flight: their 4 KI spectrum taps, then per pair 4 KI filter taps
             constexpr int KI = 2;
+            if constexpr (N > 0 && N % 2 == 0) {
+                // a lane takes two adjacent bins (v, v + 1) of a row: every filter tap pair is one
+                // 16-byte load (offsets kr n1 + kc even), the spectrum taps stay 8-byte loads (the
+                // Hermitian mirror runs backwards and the half-spectrum rows are odd-length); c5
+                // 18.60 -> 18.15 ms per step (r06u)
+                constexpr int H2 = N / 2;
+                for (int i = threadIdx.x; i < a.rows * H2; i += T) {
+                    const int rr = i / H2, v = 2 * (i - (i / H2) * H2);
+                    const int u = r0 + rr;
+                    float2 h[2][4];
+                    int fo[4];
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int kr = u + (t >> 1) * m;
+                        const int krm = kr == 0 ? 0 : m1 - kr;
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            const int kc = v + e + (t & 1) * n;
+                            const bool mir = kc > half;
+                            h[e][t] = H[mir ? krm * hld + (n1 - kc) : kr * hld + kc];
+                            h[e][t].y = mir ? -h[e][t].y : h[e][t].y;
+                        }
+                        fo[t] = kr * n1 + v + (t & 1) * n;
+                    }
+                    for (int pr = 0; pr < a.npair; ++pr) {
+                        const float2* ps = a.psi2 + pr * a.pstride;
+                        wst_f4 f[4];
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) f[t] = *reinterpret_cast<const wst_f4*>(ps + fo[t]);
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
+#pragma unroll
+                            for (int t = 0; t < 4; ++t) {
+                                const float fa = e ? f[t].z : f[t].x, fb = e ? f[t].w : f[t].y;
+                                a0 = make_float2(fmaf(h[e][t].x, fa, a0.x), fmaf(h[e][t].y, fa, a0.y));
+                                a1 = make_float2(fmaf(h[e][t].x, fb, a1.x), fmaf(h[e][t].y, fb, a1.y));
+                            }
+                            A[(2 * pr * a.rows + rr) * ld + v + e] = a0;
+                            if (2 * pr + 1 < a.npath) A[((2 * pr + 1) * a.rows + rr) * ld + v + e] = a1;
+                        }
+                    }
+                }
+            } else
             for (int i0 = threadIdx.x; i0 < a.rows * n; i0 += KI * T) {
                 float2 h[KI][4];
                 int fo[KI][4];
