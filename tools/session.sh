@@ -9,6 +9,7 @@
 #   env=<name>:<lib>:<geom>[:VAR=v+...] per-kernel ms of one library under env settings (diagnostic
 #                                       builds read WST_* knobs)
 #   km=<geom>:<chunk>[,<chunk>...][:<lib>]  per-kernel ms at several chunk sizes (planes per chunk)
+#   abl=<geom>:<mask>[,<mask>...]      phase ablation (tools/ablate.py, diagnostic build libwst_hip_diag.so)
 #   pat=<lib>[,<lib>...]               c5-geometry structured-pattern errors per build (tools/pattern_check.py)
 #   sq=<geom>[:<lib>]                   SQ counter passes of one forward (tools/pmc.sh) -> <tag>_sq summary
 #   evidence=<cfg>[,<cfg>...]           round evidence (tools/round_evidence.sh)
@@ -40,6 +41,11 @@ for step in "$@"; do
       AB_LIB=$lib WST_KM_GEOM=$geom timeout -k 10 300 python3 tools/kernel_ms.py ${chunks//,/ } > $o/${tag}_km.txt 2>&1 \
         || { echo "km failed"; tail -3 $o/${tag}_km.txt; exit 99; }
       cat $o/${tag}_km.txt ;;
+    abl)
+      IFS=: read -r geom masks <<< "$arg"
+      WST_KM_GEOM=$geom timeout -k 10 600 python3 tools/ablate.py ${masks//,/ } > $o/${tag}_abl.txt 2>&1 \
+        || { echo "abl failed"; tail -3 $o/${tag}_abl.txt; exit 99; }
+      cat $o/${tag}_abl.txt ;;
     pat)
       for lib in ${arg//,/ }; do
         AB_LIB=$lib timeout -k 10 200 python3 tools/pattern_check.py > $o/${tag}_pat_$lib.txt 2>&1 \

@@ -1283,6 +1283,39 @@ __device__ __forceinline__ void copy_to_lds(float2* dst, const float2* __restric
 template <int S>
 __device__ __forceinline__ void fold1(const float2* __restrict__ X, const float* __restrict__ psi0,
                                       int PN, float2* A, int ld1, int nM1, int nN1, int s_rt) {
+    if constexpr (S == 1) {
+        if ((nN1 & 1) == 0) {
+            // s = 1: element pairs (v, v + 1) per lane, Xhat as 16-byte loads (offsets even), the
+            // filter as 8-byte ones; U pairs per thread in flight (f3 k_o1 j1 = 0 0.790 -> 0.736 ms,
+            // c1 0.632 -> 0.596; profiles/r06_ab.txt r06y)
+            constexpr int U = 4;
+            const int T = blockDim.x;
+            const int nh = nN1 >> 1, items = nM1 * nh;
+            const wstfft::FastDiv dn(nh);
+            for (int it0 = threadIdx.x; it0 < items; it0 += U * T) {
+                float4 xv[U];
+                float2 f[U];
+                int dst[U];
+#pragma unroll
+                for (int k = 0; k < U; ++k) {
+                    const int it = it0 + k * T;
+                    const int ic = min(it, items - 1);
+                    const int u = dn.div(ic), v = 2 * (ic - u * nh);
+                    const int idx = u * PN + v;
+                    xv[k] = *reinterpret_cast<const float4*>(X + idx);
+                    f[k] = *reinterpret_cast<const float2*>(psi0 + idx);
+                    dst[k] = it < items ? u * ld1 + v : -1;
+                }
+#pragma unroll
+                for (int k = 0; k < U; ++k)
+                    if (dst[k] >= 0) {
+                        A[dst[k]] = make_float2(xv[k].x * f[k].x, xv[k].y * f[k].x);
+                        A[dst[k] + 1] = make_float2(xv[k].z * f[k].y, xv[k].w * f[k].y);
+                    }
+            }
+            return;
+        }
+    }
     const int s = (S > 0) ? S : s_rt;
     const int items = nM1 * nN1;
     const int T = blockDim.x;
@@ -1437,12 +1470,29 @@ __device__ __forceinline__ void fold2(const float2* __restrict__ H, int hld, int
     const int total = npair * items;
     const wstfft::FastDiv ditems(items), dn(nN2);
     const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, static_cast<int>(npair * pstride * 8));
+    // the next bin's box header is loaded while this bin's taps are summed (c5 k_o2 j1 = 0
+    // 9.84 -> 9.54 ms; profiles/r06_ab.txt r06z)
+    int rbn = 0, cbn = 0;
+    if (threadIdx.x < total) {
+        const int pr = ditems.div(threadIdx.x);
+        const int it = threadIdx.x - pr * items;
+        const int u = dn.div(it), v = it - u * nN2;
+        rbn = box[pr * bstride + u];
+        cbn = box[pr * bstride + nM2 + v];
+    }
     for (int w = threadIdx.x; w < total; w += blockDim.x) {
         const int pr = ditems.div(w);
         const int it = w - pr * items;
         const int u = dn.div(it), v = it - u * nN2;
-        const int* bx = box + pr * bstride;
-        const int rb = bx[u], cb = bx[nM2 + v];
+        const int rb = rbn, cb = cbn;
+        const int wn = w + blockDim.x;
+        if (wn < total) {
+            const int prn = ditems.div(wn);
+            const int itn = wn - prn * items;
+            const int un = dn.div(itn), vn = itn - un * nN2;
+            rbn = box[prn * bstride + un];
+            cbn = box[prn * bstride + nM2 + vn];
+        }
         const int i0 = rb & 255, ni = rb >> 8, j0 = cb & 255, nj = cb >> 8;
         const int fpr = static_cast<int>(pr * pstride);
         float2 a0 = make_float2(0.f, 0.f), a1 = make_float2(0.f, 0.f);
