@@ -1766,17 +1766,22 @@ __device__ __forceinline__ void fold2_tile_s2(const float2* __restrict__ H, cons
 // stage-A result in place of the batch rows (B is never written by a separate fold pass and read
 // back).  Offsets relative to the unit's bases are compile-time immediates: direct
 // db + (NB e) (+ N2 HLD for a = 1), mirrored mb + NB (NA-1-e) (+ N2 HLD for a = 0) with mb at the
-// unit's largest column, filters fo + NB e (+ N2 N1 / N2 / N2 N1 + N2).  Stage B follows after a
+// unit's largest column, filters xo + 32 NB e (the four aliases as two 16-byte loads of the
+// alias-interleaved copy).  Stage B follows after a
 // barrier (fft_lines_dr_stageB).
+// The filters come from the pairs' alias-interleaved copy psx (host: wst_hip.hip psi2): two
+// 16-byte loads per bin instead of four 8-byte ones (c2 k_o2 j1 = 0 -1 %; r06_ab.txt r06g3).
 template <int N1>
 __device__ __forceinline__ void fold2_s2_rowA(const float2* __restrict__ H, const float2* __restrict__ psi2,
                                               int npair, int npath, float2* __restrict__ B,
-                                              const float2* __restrict__ tw) {
+                                              const float2* __restrict__ tw,
+                                              const float2* __restrict__ psx) {
     constexpr int N2 = N1 / 2, HLD = N1 / 2 + 1, LD2 = N2 | 1, PSLOT = N2 * LD2, PST = N1 * N1;
     using F = wstfft::LineFFT<N2, true, fused_row_n2(N2)>;
     static_assert(F::N2 > 1, "two-stage row sizes only");
     constexpr int NA = F::N1, NB = F::N2, UNITS = N2 * NB;
-    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, npair * PST * 8);
+    (void)psi2;
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psx, npair * PST * 8);
     const char* Hb = reinterpret_cast<const char*>(H);
     // opaque start index: keeps the compiler from hoisting the unit's bases and twiddles out of
     // the caller's batch loop (live across the whole level, they pushed k_o2 into spills)
@@ -1794,16 +1799,16 @@ __device__ __forceinline__ void fold2_s2_rowA(const float2* __restrict__ H, cons
             if (g < 32) u = 8 * (g & 3) + (g >> 2);
         const int db = (u * HLD + n2) * 8;
         const int mb = ((N2 - u) * HLD + (NB - n2)) * 8;
-        const int fo = (u * N1 + n2 + pr * PST) * 8;   // lanes of a wave may straddle pairs
+        const int xo = ((u * N2 + n2) * 4 + pr * PST) * 8;   // lanes of a wave may straddle pairs
         float2 x0[NA], x1[NA];
         wstfft::static_for<0, NA>([&](auto ec) {
             constexpr int e = decltype(ec)::value;
             constexpr int dv = NB * e, dm = NB * (NA - 1 - e);
             const float2 h0 = lds_at(Hb, db + dv * 8), h1 = lds_at(Hb, db + (N2 * HLD + dv) * 8);
             const float2 m0 = lds_at(Hb, mb + (N2 * HLD + dm) * 8), m1 = lds_at(Hb, mb + dm * 8);
-            const float2 f0 = buf_load2(rs, fo, dv * 8), f1 = buf_load2(rs, fo, (N2 * N1 + dv) * 8);
-            const float2 g0 = buf_load2(rs, fo, (N2 + dv) * 8);
-            const float2 g1 = buf_load2(rs, fo, (N2 * N1 + N2 + dv) * 8);
+            const float4 A = buf_load4(rs, xo, dv * 32), Bq = buf_load4(rs, xo, dv * 32 + 16);
+            const float2 f0 = make_float2(A.x, A.y), f1 = make_float2(A.z, A.w);
+            const float2 g0 = make_float2(Bq.x, Bq.y), g1 = make_float2(Bq.z, Bq.w);
             x0[e].x = fmaf(h0.x, f0.x, fmaf(h1.x, f1.x, fmaf(m0.x, g0.x, m1.x * g1.x)));
             x0[e].y = fmaf(h0.y, f0.x, fmaf(h1.y, f1.x, fmaf(-m0.y, g0.x, -m1.y * g1.x)));
             x1[e].x = fmaf(h0.x, f0.y, fmaf(h1.x, f1.y, fmaf(m0.x, g0.y, m1.x * g1.y)));
@@ -2372,7 +2377,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
             const int* bx = p.box + p.box_off[j2 * J + j1] + (l2a >> 1) * (nM2 + nN2);
             if (!(dbg & 8) && !(dbg & (s2 == 2 ? 256 : 512))) {
                 if constexpr (FUSE) {
-                    fold2_s2_rowA<N1F>(H, ps, npair, npath, B, tb.twN(j2));
+                    fold2_s2_rowA<N1F>(H, ps, npair, npath, B, tb.twN(j2), ps + nq * pstride);
                 } else if constexpr (N1F > 0 && SC == 2) {
                     fold2_tile_s2<N1F>(H, ps, npair, npath, B);
                 } else if constexpr (N1F > 0 && (SC == 4 || SC == 8)) {

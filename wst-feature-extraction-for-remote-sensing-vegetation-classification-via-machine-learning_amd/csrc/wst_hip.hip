@@ -553,7 +553,7 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
     std::vector<long long> psi2_off(static_cast<size_t>(J) * J * nq, -1);
     if (max_order >= 2 && device) {
         for (int j2 = 1; j2 < J; ++j2)
-            for (int r = 0; r < j2 && r < wst::psi_levels(j2, J); ++r)
+            for (int r = 0; r < j2 && r < wst::psi_levels(j2, J); ++r) {
                 for (int q = 0; q < nq; ++q) {
                     psi2_off[(static_cast<size_t>(j2) * J + r) * nq + q] = static_cast<long long>(psi2.size());
                     const size_t nb = static_cast<size_t>(g.PM >> r) * (g.PN >> r);
@@ -566,6 +566,28 @@ int create_plan(int M, int N, int J, int L, int max_order, int pre_pad,
                         psi2.push_back(make_float2(v[0], v[1]));
                     }
                 }
+                // s = 2 level (r = j2 - 1) of a square plane: an alias-interleaved copy of every pair
+                // after the (j2, r) block (pair q at psi2_off[(j2, r, 0)] + (nq + q) n^2): per folded
+                // bin (u, v) the aliases (u, v), (u + n/2, v), (u, v + n/2), (u + n/2, v + n/2) -- two
+                // 16-byte loads in fold2_s2_rowA (the other folds read the plain blocks)
+                const int n = g.PM >> r;
+                if (r == j2 - 1 && g.PM == g.PN && n % 2 == 0) {
+                    const int h = n / 2;
+                    const size_t base = static_cast<size_t>(psi2_off[(static_cast<size_t>(j2) * J + r) * nq]);
+                    for (int q = 0; q < nq; ++q) {
+                        const size_t b = base + static_cast<size_t>(q) * n * n;
+                        for (int u = 0; u < h; ++u)
+                            for (int v = 0; v < h; ++v) {
+                                const size_t i0 = b + static_cast<size_t>(u) * n + v, i1 = i0 + static_cast<size_t>(h) * n;
+                                const float2 a0 = psi2[i0], a1 = psi2[i1], a2 = psi2[i0 + h], a3 = psi2[i1 + h];
+                                psi2.push_back(a0);
+                                psi2.push_back(a1);
+                                psi2.push_back(a2);
+                                psi2.push_back(a3);
+                            }
+                    }
+                }
+            }
     }
     // alias boxes of the order-2 pairs (see fold2): per (j2, r) all pairs, stride nM2 + nN2
     std::vector<int> box;
