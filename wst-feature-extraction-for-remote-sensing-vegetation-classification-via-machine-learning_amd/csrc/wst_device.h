@@ -1446,6 +1446,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* base,
 __device__ __forceinline__ float2 buf_load2(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
     return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
 }
+__device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
 
 // Order-2 Hermitian fold of npair filter pairs (2 paths each) into B:
 //   B_b[u][v] = sum_{i,j < s} U1hat[u + i nM2][v + j nN2] * psi_b[...]
@@ -1549,7 +1552,9 @@ __device__ __forceinline__ void fold2(const float2* __restrict__ H, int hld, int
 // (pair, u) of the batch in steps of rpp = T / nN2 (lanes beyond rpp * nN2 idle); the filter
 // taps come through a buffer descriptor with the row offsets as wave-uniform soffsets.
 // R rows of a lane in flight per iteration (R = 2 when H is read from HBM / L2: HG kernels).
-template <int R = 1>
+// X: the filters from the pairs' alias-interleaved copy (square planes; host: wst_hip.hip psi2),
+// the four aliases of a bin as two 16-byte loads.
+template <int R = 1, bool X = false>
 __device__ __forceinline__ void fold2_s2(const float2* __restrict__ H, int hld, int nM1, int nN1,
                                          const float2* __restrict__ psi2, long long pstride,
                                          int npair, int npath, float2* __restrict__ B, int pslot,
@@ -1582,11 +1587,21 @@ __device__ __forceinline__ void fold2_s2(const float2* __restrict__ H, int hld, 
             h[r][1] = H[hm0 + cB];
             h[r][2] = H[hr + hq + v];
             h[r][3] = H[hm1 + cB];
-            const int fo = (static_cast<int>(pr[r] * pstride) + u * nN1 + v) * 8;
-            f[r][0] = buf_load2(rs, fo, 0);
-            f[r][1] = buf_load2(rs, fo, nN2 * 8);
-            f[r][2] = buf_load2(rs, fo, fq);
-            f[r][3] = buf_load2(rs, fo, fq + nN2 * 8);
+            if constexpr (X) {
+                // psi2 points at the copy: aliases (u, v), (u + nM2, v), (u, v + nN2), (u + nM2, v + nN2)
+                const int xo = (static_cast<int>(pr[r] * pstride) + (u * nN2 + v) * 4) * 8;
+                const float4 A = buf_load4(rs, xo, 0), Bq = buf_load4(rs, xo, 16);
+                f[r][0] = make_float2(A.x, A.y);
+                f[r][2] = make_float2(A.z, A.w);
+                f[r][1] = make_float2(Bq.x, Bq.y);
+                f[r][3] = make_float2(Bq.z, Bq.w);
+            } else {
+                const int fo = (static_cast<int>(pr[r] * pstride) + u * nN1 + v) * 8;
+                f[r][0] = buf_load2(rs, fo, 0);
+                f[r][1] = buf_load2(rs, fo, nN2 * 8);
+                f[r][2] = buf_load2(rs, fo, fq);
+                f[r][3] = buf_load2(rs, fo, fq + nN2 * 8);
+            }
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -1609,9 +1624,6 @@ __device__ __forceinline__ void fold2_s2(const float2* __restrict__ H, int hld, 
 // Two adjacent columns (v, v + 1) per lane (even nN2): the filter taps of both as one 16-byte
 // buffer load (offsets (pr pstride + u nN1 + v) even), the spectrum taps 8-byte (the mirror runs
 // backwards over odd-length rows); rows walked in steps of T / (nN2 / 2).
-__device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-}
 template <int R = 1>
 __device__ __forceinline__ void fold2_s2_pairs(const float2* __restrict__ H, int hld, int nM1, int nN1,
                                                const float2* __restrict__ psi2, long long pstride,
@@ -1689,7 +1701,8 @@ template <int R = 1>
 __device__ __forceinline__ void fold2_any(int s2, const float2* H, int hld, int nM1, int nN1,
                                           const float2* psi2, long long pstride, int npair,
                                           int npath, float2* B, int pslot, int ld2, int nM2,
-                                          int nN2, const int* box, int bstride) {
+                                          int nN2, const int* box, int bstride,
+                                          const float2* psx = nullptr) {
     if (s2 == 2) {
         // column pairs where they keep > 6 % more lanes busy (f3's 68-column paths on 512 lanes:
         // 476 -> 510, k_o2 1.216 -> 1.166 ms; c1's 36 columns on 256 lanes gain no lanes and
@@ -1698,6 +1711,8 @@ __device__ __forceinline__ void fold2_any(int s2, const float2* H, int hld, int 
         const int T = blockDim.x;
         if (R == 2 && (nN2 & 1) == 0 && (T / (nN2 >> 1)) * (nN2 >> 1) * 100 > (T / nN2) * nN2 * 106)
             fold2_s2_pairs<1>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
+        else if (psx)   // c1 k_o2 1.192 -> 1.153 ms, c5 HG j1 = 1 2.19 -> 2.12 ms (r06_ab.txt r06g4)
+            fold2_s2<R, true>(H, hld, nM1, nN1, psx, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
         else
             fold2_s2<R>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
     }
@@ -1726,11 +1741,13 @@ __device__ __forceinline__ cint_p to_const_as(const T* p) {
 
 template <int N1>
 __device__ __forceinline__ void fold2_tile_s2(const float2* __restrict__ H, const float2* __restrict__ psi2,
-                                              int npair, int npath, float2* __restrict__ B) {
+                                              int npair, int npath, float2* __restrict__ B,
+                                              const float2* __restrict__ psx) {
     constexpr int N2 = N1 / 2, HLD = N1 / 2 + 1, LD2 = N2 | 1, PSLOT = N2 * LD2;
     constexpr int ITEMS = N2 * N2, NT = (ITEMS + 63) / 64, PST = N1 * N1;
     const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psi2, npair * PST * 8);
+    (void)psi2;   // the filters from the alias-interleaved copy (c2 k_o2 j1 = 1 0.475 -> 0.454 ms; r06g5)
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(psx, npair * PST * 8);
     const char* Hb = reinterpret_cast<const char*>(H);
     const int w0 = wave_id();
     for (int k = 0;; ++k) {
@@ -1742,11 +1759,13 @@ __device__ __forceinline__ void fold2_tile_s2(const float2* __restrict__ H, cons
         const int bin = min(bin0, ITEMS - 1);
         const int u = bin / N2, v = bin - u * N2;
         const int db = (u * HLD + v) * 8, mb = ((N2 - u) * HLD + (N2 - v)) * 8;
-        const int fo = (u * N1 + v) * 8, po = pr * PST * 8;
+        const int po = pr * PST * 8;
         const float2 h0 = lds_at(Hb, db), h1 = lds_at(Hb, db + N2 * HLD * 8);   // (0,0) (1,0)
         const float2 m0 = lds_at(Hb, mb + N2 * HLD * 8), m1 = lds_at(Hb, mb);   // (0,1) (1,1)
-        const float2 f0 = buf_load2(rs, fo, po), f1 = buf_load2(rs, fo, po + N2 * N1 * 8);
-        const float2 g0 = buf_load2(rs, fo, po + N2 * 8), g1 = buf_load2(rs, fo, po + (N2 * N1 + N2) * 8);
+        const int xo = (u * N2 + v) * 32;
+        const float4 A = buf_load4(rs, xo, po), Bq = buf_load4(rs, xo, po + 16);
+        const float2 f0 = make_float2(A.x, A.y), f1 = make_float2(A.z, A.w);
+        const float2 g0 = make_float2(Bq.x, Bq.y), g1 = make_float2(Bq.z, Bq.w);
         float2 a0, a1;
         a0.x = fmaf(h0.x, f0.x, fmaf(h1.x, f1.x, fmaf(m0.x, g0.x, m1.x * g1.x)));
         a0.y = fmaf(h0.y, f0.x, fmaf(h1.y, f1.x, fmaf(-m0.y, g0.x, -m1.y * g1.x)));
@@ -2379,14 +2398,15 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                 if constexpr (FUSE) {
                     fold2_s2_rowA<N1F>(H, ps, npair, npath, B, tb.twN(j2), ps + nq * pstride);
                 } else if constexpr (N1F > 0 && SC == 2) {
-                    fold2_tile_s2<N1F>(H, ps, npair, npath, B);
+                    fold2_tile_s2<N1F>(H, ps, npair, npath, B, ps + nq * pstride);
                 } else if constexpr (N1F > 0 && (SC == 4 || SC == 8)) {
                     constexpr int NT = ((N1F / SC) * (N1F / SC) + 63) / 64;
                     fold2_tile_list<N1F, SC>(H, ps, npair, npath, B,
                                              p.taph + p.taph_off[j2 * J + j1] + (l2a >> 1) * NT, p.taps);
                 } else {
+                    // the alias-interleaved copy exists for every s = 2 level of a square plane
                     fold2_any<HG ? 2 : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2,
-                                          nN2, bx, nM2 + nN2);
+                                          nN2, bx, nM2 + nN2, p.PM == p.PN ? ps + nq * pstride : nullptr);
                 }
             }
             __syncthreads();
