@@ -1551,7 +1551,7 @@ __device__ __forceinline__ void fold2(const float2* __restrict__ H, int hld, int
 // Each lane keeps one column v (its mirror column and sign are fixed) and walks the rows
 // (pair, u) of the batch in steps of rpp = T / nN2 (lanes beyond rpp * nN2 idle); the filter
 // taps come through a buffer descriptor with the row offsets as wave-uniform soffsets.
-// R rows of a lane in flight per iteration (R = 2 when H is read from HBM / L2: HG kernels).
+// R rows of a lane in flight per iteration (R = 3 when H is read from HBM / L2: HG kernels).
 // X: the filters from the pairs' alias-interleaved copy (square planes; host: wst_hip.hip psi2),
 // the four aliases of a bin as two 16-byte loads.
 template <int R = 1, bool X = false>
@@ -1707,9 +1707,11 @@ __device__ __forceinline__ void fold2_any(int s2, const float2* H, int hld, int 
         // column pairs where they keep > 6 % more lanes busy (f3's 68-column paths on 512 lanes:
         // 476 -> 510, k_o2 1.216 -> 1.166 ms; c1's 36 columns on 256 lanes gain no lanes and
         // measured 1.3 % slower, c5's 96 on 1024 +5 % lanes, neutral; profiles/r06_ab.txt r06w),
-        // one row pair per lane in flight (two: 0.6 % slower, three: 4 %; r06x)
+        // one row pair per lane in flight (two: 0.6 % slower, three: 4 %; r06x); the dense form
+        // with the interleaved filters takes R = 3 rows per lane in flight for HG (c1 k_o2 1.18 ->
+        // 1.135 ms, c5 HG j1 = 1 2.17 -> 2.08 ms against R = 2; r06g8)
         const int T = blockDim.x;
-        if (R == 2 && (nN2 & 1) == 0 && (T / (nN2 >> 1)) * (nN2 >> 1) * 100 > (T / nN2) * nN2 * 106)
+        if (R >= 2 && (nN2 & 1) == 0 && (T / (nN2 >> 1)) * (nN2 >> 1) * 100 > (T / nN2) * nN2 * 106)
             fold2_s2_pairs<1>(H, hld, nM1, nN1, psi2, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
         else if (psx)   // c1 k_o2 1.192 -> 1.153 ms, c5 HG j1 = 1 2.19 -> 2.12 ms (r06_ab.txt r06g4)
             fold2_s2<R, true>(H, hld, nM1, nN1, psx, pstride, npair, npath, B, pslot, ld2, nM2, nN2);
@@ -2405,7 +2407,7 @@ __device__ __forceinline__ void k_o2_body(unsigned char* smem, const DevParams& 
                                              p.taph + p.taph_off[j2 * J + j1] + (l2a >> 1) * NT, p.taps);
                 } else {
                     // the alias-interleaved copy exists for every s = 2 level of a square plane
-                    fold2_any<HG ? 2 : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2,
+                    fold2_any<HG ? 3 : 1>(s2, H, hld, nM1, nN1, ps, pstride, npair, npath, B, pslot, ld2, nM2,
                                           nN2, bx, nM2 + nN2, p.PM == p.PN ? ps + nq * pstride : nullptr);
                 }
             }
