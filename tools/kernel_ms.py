@@ -12,21 +12,22 @@ B, M, J = _g[:3]
 LL = _g[3] if len(_g) > 3 else 8
 x = torch.from_numpy(np.random.default_rng(1).integers(0, 256, (B, M, M), dtype=np.uint8).astype(np.float32) / 255).cuda()
 plan = _lib.Plan(M, M, J, LL)
-out = torch.empty((B, plan.K, plan.Mo, plan.No), device="cuda")
+POOLED = os.environ.get("KM_POOLED") == "1"   # pooled mean / std output (the reference's features)
+out = torch.empty((B, 2 * plan.K) if POOLED else (B, plan.K, plan.Mo, plan.No), device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 nslot = 1 + 2 * J
 for chunk in [int(a) for a in sys.argv[1:]] or [2048]:
     wsb = plan.workspace_bytes(chunk); ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
-    for _ in range(2): plan.forward(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st)
+    for _ in range(2): plan.forward(x.data_ptr(), B, out.data_ptr(), POOLED, ws.data_ptr(), wsb, st)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(10): plan.forward(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st)
+    for _ in range(10): plan.forward(x.data_ptr(), B, out.data_ptr(), POOLED, ws.data_ptr(), wsb, st)
     e1.record(); torch.cuda.synchronize()
     wall = e0.elapsed_time(e1) / 10
     acc = [0.0] * nslot
     for _ in range(5):
-        ms = plan.forward_profiled(x.data_ptr(), B, out.data_ptr(), False, ws.data_ptr(), wsb, st, nslot)
+        ms = plan.forward_profiled(x.data_ptr(), B, out.data_ptr(), POOLED, ws.data_ptr(), wsb, st, nslot)
         acc = [a + b for a, b in zip(acc, ms)]
     acc = [round(a / 5, 3) for a in acc]
     print(os.environ.get("AB_LIB", "default"), f"chunk={chunk} wall={wall:.3f} ms",
